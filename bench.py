@@ -1,0 +1,291 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident halo pack+unpack GB/s (BASELINE.json metric) on MI355X.
+
+Workload (BASELINE configs[1], weak-scaled for N>1 as configs[2]): per GPU one 512^3 fp64 domain
+(extent 516^3 with halo 2), 26-neighbour periodic halo. N=1: one periodic domain (all 26
+iteration spaces are a self message); N=2/4/8: (2,1,1)/(2,2,1)/(2,2,2) decomposition of the
+periodic global grid, one rank per GPU.
+
+A step = one fused pack launch (every iteration space of every send buffer) + one fused unpack
+launch (every recv buffer), with fields and buffers resident in HBM. Algorithmic bytes per step
+per GPU = 4 * n * 8 (pack read + write, unpack read + write), n = (N+2H)^3 - N^3 halo cells.
+value = sum over ranks of bytes*K / max over ranks of the K-step wall time.
+
+Before timing, one full exchange (pack -> RCCL send/recv over xGMI for N>1 -> unpack) is run and
+every cell of every rank's (N+2H)^3 box is verified on the GPU against the wrapped global index.
+Extra fields: the full exchange time (incl. RCCL), the host-staged rate (pack + D2H + H2D +
+unpack through pinned memory), per-kernel HIP-event durations, and on rank 0 at N=1 the oracle's
+single-thread CPU pack+unpack on a bounded sample (cpu_baseline).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident halo pack+unpack GB/s, 512^3 fp64 halo=2, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+DECOMP = {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2)}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--N", type=int, default=512)
+    p.add_argument("--halo", type=int, default=2)
+    p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import ghex_amd
+    from ghex_amd import _ghx
+    from ghex_amd.structured import regular as R
+    ghex_amd.native_library()
+
+    N, Hw = args.N, args.halo
+    E = N + 2 * Hw
+    parts = DECOMP[world]
+    G = [parts[d] * N for d in range(3)]
+    c = (rank % parts[0], (rank // parts[0]) % parts[1], rank // (parts[0] * parts[1]))
+    first = tuple(c[d] * N for d in range(3))
+    last = tuple((c[d] + 1) * N - 1 for d in range(3))
+
+    ctx = ghex_amd.make_context()
+    dd = R.DomainDescriptor(rank, first, last)
+    hg = R.HaloGenerator((0, 0, 0), tuple(g - 1 for g in G), (Hw,) * 6, (True,) * 3)
+    pc = R.make_pattern(ctx, hg, [dd])
+
+    # synthetic field: owned cell = global linear index (exact in fp64), halo = -1
+    base = torch.full((E, E, E), -1.0, dtype=torch.float64, device=dev)
+    ar = [torch.arange(N, device=dev, dtype=torch.float64) + first[d] for d in range(3)]
+    base[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = (
+        ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)))
+    logical = base.permute(2, 1, 0)  # (x, y, z), x contiguous: layout_map<2,1,0>
+    fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (E,) * 3)
+    co = R.make_communication_object(ctx)
+    bis = [pc(fd)]
+
+    # ---- verified full exchange (pack -> RCCL -> unpack) --------------------------------------
+    co.exchange(bis).wait()
+    idx = [torch.arange(E, device=dev, dtype=torch.int64) - Hw + first[d] for d in range(3)]
+    wrap = [(idx[d] % G[d]).to(torch.float64) for d in range(3)]
+    expect = wrap[0].view(1, 1, E) + G[0] * (wrap[1].view(1, E, 1) + G[1] * wrap[2].view(E, 1, 1))
+    bad = int((base != expect).sum().item())
+    del expect
+    verified = bad == 0
+    if world > 1:
+        t = torch.tensor([bad], device=dev)
+        dist.all_reduce(t)
+        verified = int(t.item()) == 0
+
+    plan = co.plan(bis)
+    send, recv = co.buffers(plan, dev)
+    n_halo = E ** 3 - N ** 3
+    step_bytes = 4 * n_halo * 8
+    assert sum(b["size"] for b in plan.send) == n_halo * 8
+    stream = torch.cuda.current_stream(dev)
+    fptr = _ghx.ptr_array([fd.data_ptr()])
+    sptr = _ghx.ptr_array([t.data_ptr() for t in send])
+    rptr = _ghx.ptr_array([t.data_ptr() for t in recv])
+    L = _ghx.lib()
+    ns, nr = len(send), len(recv)
+
+    def pack(s):
+        rc = L.ghx_exchange_pack(plan.h, fptr, 1, sptr, ns, s)
+        if rc:
+            raise RuntimeError(L.ghx_last_error().decode())
+
+    def unpack(s):
+        rc = L.ghx_exchange_unpack(plan.h, fptr, 1, rptr, nr, s)
+        if rc:
+            raise RuntimeError(L.ghx_last_error().decode())
+
+    def step():
+        s = torch.cuda.current_stream(dev).cuda_stream
+        pack(s)
+        unpack(s)
+
+    graph = None
+    if not args.no_graph:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            step()  # warm the capture stream
+        stream.wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+    run = graph.replay if graph is not None else step
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize(dev)
+
+    def timed(fn, k):
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        dt = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        return dt
+
+    K = args.steps
+    T = timed(run, K)
+    value = world * step_bytes * K / T / 1e9
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+        "steps": K, "warmup": args.warmup, "ms_per_step": round(T / K * 1e3, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (owned cell = global linear index; verified after a full exchange)",
+        "config": {
+            "workload": f"{N}^3 fp64 structured 3D halo={Hw}, 26-neighbour periodic, "
+                        f"device-resident pack+unpack, decomposition {list(parts)}",
+            "N": N, "halo": Hw, "fields": 1, "decomposition": list(parts),
+            "launch": "hipGraph" if graph is not None else "eager",
+            "bytes_per_step_per_gpu": step_bytes,
+            "parallelism": f"{world} rank(s), one domain per GPU",
+        },
+        "verified": verified,
+    }
+
+    # ---- per-kernel HIP-event durations (dominant kernel roofline) ----------------------------
+    kk = min(K, 100)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(kk)]
+    torch.cuda.synchronize(dev)
+    for i in range(kk):
+        s = torch.cuda.current_stream(dev).cuda_stream
+        ev[i][0].record(stream)
+        pack(s)
+        ev[i][1].record(stream)
+        ev[i][2].record(stream)
+        unpack(s)
+        ev[i][3].record(stream)
+    torch.cuda.synchronize(dev)
+    t_pack = sum(e[0].elapsed_time(e[1]) for e in ev) / kk * 1e-3
+    t_unpack = sum(e[2].elapsed_time(e[3]) for e in ev) / kk * 1e-3
+    launch_bytes = 2 * n_halo * 8
+    dom_name, dom_t = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+    achieved = launch_bytes / dom_t / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            ent = tj.get(f"N{N}_H{Hw}", {}).get(dom_name)
+            traffic = ent.get("hbm_bytes_per_launch") if ent else None
+        except Exception:
+            traffic = None
+    out["roofline"] = {"bound": "hbm", "kernel": f"k_structured<{dom_name}>",
+                       "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                       "algorithmic_bytes_per_launch": launch_bytes,
+                       "pack_us": round(t_pack * 1e6, 2), "unpack_us": round(t_unpack * 1e6, 2)}
+
+    if not args.no_extras:
+        # full exchange incl. transport (RCCL for N>1; self-message aliasing for N=1)
+        ke = min(K, 50)
+        for _ in range(3):
+            co.exchange(bis).wait()
+        Te = timed(lambda: co.exchange(bis).wait(), ke)
+        out["exchange_ms_per_step"] = round(Te / ke * 1e3, 4)
+        # host-staged: pack -> D2H (pinned) -> H2D -> unpack (NIC-side buffers, north star)
+        hs = [torch.empty(b["size"], dtype=torch.uint8, pin_memory=True) for b in plan.send]
+
+        def staged():
+            s = torch.cuda.current_stream(dev).cuda_stream
+            pack(s)
+            for i, b in enumerate(plan.send):
+                hs[i].copy_(send[i][:b["size"]], non_blocking=True)
+            for i, b in enumerate(plan.recv):  # N=1: every message is a self message
+                j = next(j for j, x in enumerate(plan.send) if x["pair"] == b["pair"])
+                recv[i][:b["size"]].copy_(hs[j], non_blocking=True)
+            unpack(s)
+
+        if world == 1:
+            for _ in range(3):
+                staged()
+            Ts = timed(staged, min(K, 50))
+            pcie = 2 * n_halo * 8
+            out["host_staged"] = {
+                "GBps_algorithmic": round(step_bytes * min(K, 50) / Ts / 1e9, 2),
+                "ms_per_step": round(Ts / min(K, 50) * 1e3, 4),
+                "pcie_bytes_per_step": pcie}
+            # restore valid halos after the staged copies
+            co.exchange(bis).wait()
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, Hw, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+        dist.destroy_process_group()
+
+
+def cpu_baseline(N, Hw, seconds):
+    """The oracle's single-thread C restatement of serialization<cpu>::pack_batch/unpack_batch
+    (include/ghex/structured/pack_kernels.hpp:62-158) on the same workload, bounded in time."""
+    import numpy as np
+    from oracle import oracle as orc
+    E = N + 2 * Hw
+    a = np.zeros((E, E, E))
+    a[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = np.arange(N ** 3, dtype=np.float64).reshape(N, N, N)
+    dom = orc.RegularDomain(0, (0, 0, 0), (N - 1,) * 3)
+    pat = orc.regular_make_pattern([[dom]], (0, 0, 0), (N - 1,) * 3, (Hw,) * 6, (1, 1, 1))[0][0]
+    spec = orc.FieldSpec(a, 8, (2, 1, 0), (Hw,) * 3, (E,) * 3)
+    send = list(pat.send.values())[0][1]
+    recv = list(pat.recv.values())[0][1]
+    nbytes = sum(b.size() for b in send) * 8
+    buf = np.zeros(nbytes, np.uint8)
+    orc.structured_pack(spec, buf, send)
+    orc.structured_unpack(spec, buf, recv)
+    t0 = time.perf_counter()
+    it = 0
+    while True:
+        orc.structured_pack(spec, buf, send)
+        orc.structured_unpack(spec, buf, recv)
+        it += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds and it >= 3:
+            break
+    gbs = 4 * nbytes * it / dt / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{N}^3 fp64 H={Hw} one periodic domain, pack+unpack x{it} "
+                      f"({dt:.1f} s, 1 thread, oracle/ghex_oracle.c row-memcpy restatement)"}
+
+
+if __name__ == "__main__":
+    main()

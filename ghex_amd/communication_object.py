@@ -1,0 +1,221 @@
+"""communication_object — the exchange of the halo path
+(include/ghex/communication_object.hpp:271-285, 483-828) on MI355X.
+
+exchange(buffer_infos):
+  1. plan (cached per field set): buffers per domain pair, fields in argument order with
+     alignof padding, tags = pattern tag + per-container offset (communication_object::allocate,
+     :1003-1067) — done in libghx (ghx_exchange_create);
+  2. ONE fused pack launch for all send buffers on the current stream;
+  3. transport: self-messages are not sent — the unpack reads the send buffer directly
+     (SURVEY §8(e)); peer messages go through torch.distributed point-to-point (backend
+     "nccl" = RCCL over xGMI), posted as one group (batch_isend_irecv), stream-ordered like the
+     reference's stream-aware branch (:703-714, 751-765);
+  4. ONE fused unpack launch for all recv buffers.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Sequence
+
+from . import _ghx
+
+
+class _ExchangePlan:
+    def __init__(self, items: List[_ghx.ExchangeItem]):
+        arr = (_ghx.ExchangeItem * len(items))(*items)
+        h = ctypes.c_void_p()
+        _ghx.call("ghx_exchange_create", arr, len(items), ctypes.byref(h))
+        self.h = h
+        self.send = self._buffers(0)
+        self.recv = self._buffers(1)
+
+    def _buffers(self, direction):
+        n = ctypes.c_int32()
+        _ghx.call("ghx_exchange_num_buffers", self.h, direction, ctypes.byref(n))
+        out = []
+        for i in range(n.value):
+            a, b, r, t = (ctypes.c_int32() for _ in range(4))
+            s = ctypes.c_uint64()
+            _ghx.call("ghx_exchange_buffer", self.h, direction, i, ctypes.byref(a),
+                      ctypes.byref(b), ctypes.byref(r), ctypes.byref(t), ctypes.byref(s))
+            out.append(dict(pair=(a.value, b.value), rank=r.value, tag=t.value, size=s.value))
+        return out
+
+    def __del__(self):
+        try:
+            if self.h:
+                _ghx.lib().ghx_exchange_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def route(context, sends, recvs):
+    """Post one group of point-to-point messages. sends/recvs: [(peer_rank, tag, tensor)].
+
+    Messages between one pair of ranks are matched in (tag) order on both sides (NCCL/RCCL
+    matches by issue order; gloo by tag) — the tag of a send buffer equals the tag of the
+    matching recv buffer by construction of the pattern. Returns the list of works."""
+    dist = context.distributed
+    ops = []
+    for peer, tag, t in sorted(recvs, key=lambda x: (x[0], x[1])):
+        ops.append(dist.P2POp(dist.irecv, t, context.global_rank(peer), context.group, tag))
+    for peer, tag, t in sorted(sends, key=lambda x: (x[0], x[1])):
+        ops.append(dist.P2POp(dist.isend, t, context.global_rank(peer), context.group, tag))
+    if not ops:
+        return []
+    return dist.batch_isend_irecv(ops)
+
+
+class CommunicationHandle:
+    """communication_handle (communication_object.hpp:78-130): wait / is_ready / progress."""
+
+    def __init__(self, co, stream, event):
+        self._co = co
+        self._stream = stream
+        self._event = event
+
+    def wait(self):
+        if self._event is not None:
+            self._event.synchronize()
+        if self._co is not None:
+            self._co._valid = False
+            self._co = None
+
+    def is_ready(self) -> bool:
+        if self._event is None or self._event.query():
+            if self._co is not None:
+                self._co._valid = False
+                self._co = None
+            return True
+        return False
+
+    def progress(self):
+        self.is_ready()
+
+    def schedule_wait(self, stream=None):
+        """Make `stream` wait for the exchange without blocking the host
+        (communication_handle::schedule_wait, :832-856)."""
+        if self._event is not None and stream is not None:
+            stream.wait_event(self._event)
+
+
+class CommunicationObject:
+    """communication_object<grid, domain_id> (make_communication_object, :1105-1112)."""
+
+    def __init__(self, context):
+        self.context = context
+        self._plans = {}
+        self._bufs = {}
+        self._valid = False
+
+    # -- planning -----------------------------------------------------------------------------
+    def _key(self, bis):
+        k = []
+        for bi in bis:
+            f = bi.field
+            k.append((id(bi.pattern_container), bi.local_index, f.kind, bytes(f.desc), f.align))
+        return tuple(k)
+
+    def plan(self, bis):
+        key = self._key(bis)
+        p = self._plans.get(key)
+        if p is None:
+            # tag offsets per distinct pattern container (prepare_exchange_buffers :540-549)
+            offsets, acc = {}, 0
+            for bi in bis:
+                pc = bi.pattern_container
+                if id(pc) not in offsets:
+                    offsets[id(pc)] = acc
+                    acc += pc.max_tag() + 1
+            items = []
+            for bi in bis:
+                it = _ghx.ExchangeItem()
+                it.pattern = bi.pattern_container.handle
+                it.local_index = bi.local_index
+                it.kind = bi.field.kind
+                if bi.field.kind == 0:
+                    it.field = bi.field.desc
+                else:
+                    it.udata = bi.field.desc
+                it.align = bi.field.align
+                it.tag_offset = offsets[id(bi.pattern_container)]
+                items.append(it)
+            p = _ExchangePlan(items)
+            self._plans[key] = (p, [bi.pattern_container for bi in bis])
+        else:
+            p = p[0]
+        return p
+
+    def buffers(self, plan, device):
+        """Device buffers, reused across exchanges while sizes are unchanged (:581-589)."""
+        import torch
+        key = (id(plan), str(device))
+        b = self._bufs.get(key)
+        if b is None:
+            send = [torch.empty(max(1, x["size"]), dtype=torch.uint8, device=device)
+                    for x in plan.send]
+            recv = []
+            me = self.context.rank()
+            for x in plan.recv:
+                # self-message: unpack straight from the matching send buffer
+                j = next((i for i, s in enumerate(plan.send)
+                          if s["pair"] == x["pair"] and x["rank"] == me), None)
+                recv.append(send[j] if j is not None else
+                            torch.empty(max(1, x["size"]), dtype=torch.uint8, device=device))
+            b = (send, recv)
+            self._bufs[key] = b
+        return b
+
+    # -- exchange ------------------------------------------------------------------------------
+    def exchange(self, *buffer_infos) -> CommunicationHandle:
+        import torch
+        bis = list(buffer_infos[0]) if (len(buffer_infos) == 1 and
+                                         isinstance(buffer_infos[0], (list, tuple))) \
+            else list(buffer_infos)
+        if self._valid:
+            raise RuntimeError("earlier exchange operation was not finished")
+        if not bis:
+            return CommunicationHandle(None, None, None)
+        device = bis[0].field.device
+        plan = self.plan(bis)
+        send, recv = self.buffers(plan, device)
+        stream = torch.cuda.current_stream(device)
+        fptrs = _ghx.ptr_array([bi.field.data_ptr() for bi in bis])
+        sptrs = _ghx.ptr_array([t.data_ptr() for t in send])
+        rptrs = _ghx.ptr_array([t.data_ptr() for t in recv])
+        self._valid = True
+        _ghx.call("ghx_exchange_pack", plan.h, fptrs, len(bis), sptrs, len(send),
+                  stream.cuda_stream)
+        me = self.context.rank()
+        sends = [(x["rank"], x["tag"], send[i][:x["size"]]) for i, x in enumerate(plan.send)
+                 if x["rank"] != me]
+        recvs = [(x["rank"], x["tag"], recv[i][:x["size"]]) for i, x in enumerate(plan.recv)
+                 if x["rank"] != me]
+        for w in route(self.context, sends, recvs):
+            w.wait()  # stream-ordered for NCCL: the unpack below is queued behind the recvs
+        _ghx.call("ghx_exchange_unpack", plan.h, fptrs, len(bis), rptrs, len(recv),
+                  stream.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return CommunicationHandle(self, stream, ev)
+
+    # low-level access for benchmarks / tests (no transport)
+    def pack_only(self, bis, stream=None):
+        import torch
+        plan = self.plan(bis)
+        send, recv = self.buffers(plan, bis[0].field.device)
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        _ghx.call("ghx_exchange_pack", plan.h, _ghx.ptr_array([b.field.data_ptr() for b in bis]),
+                  len(bis), _ghx.ptr_array([t.data_ptr() for t in send]), len(send), s)
+        return plan, send, recv
+
+    def unpack_only(self, bis, stream=None):
+        import torch
+        plan = self.plan(bis)
+        send, recv = self.buffers(plan, bis[0].field.device)
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        _ghx.call("ghx_exchange_unpack", plan.h,
+                  _ghx.ptr_array([b.field.data_ptr() for b in bis]), len(bis),
+                  _ghx.ptr_array([t.data_ptr() for t in recv]), len(recv), s)
+        return plan, send, recv

@@ -1,0 +1,669 @@
+// ghx_abi.cpp — the extern "C" boundary (include/ghx.h): argument checks, error capture,
+// opaque handles, and the exchange planner (communication_object::allocate semantics).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <list>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <unordered_map>
+
+#include "ghx_pattern.hpp"
+#include "ghx_plan.hpp"
+
+struct ghx_pattern : ghx::pattern_set
+{
+};
+
+namespace ghx
+{
+namespace
+{
+thread_local std::string g_error;
+
+template<typename F>
+int guarded(F&& f)
+{
+    try
+    {
+        g_error.clear();
+        return f();
+    }
+    catch (const invalid& e)
+    {
+        g_error = e.what();
+        return GHX_ERR_INVALID;
+    }
+    catch (const hip_error& e)
+    {
+        g_error = std::string(e.what()) + ": " + hipGetErrorString(hipGetLastError());
+        return GHX_ERR_HIP;
+    }
+    catch (const std::bad_alloc&)
+    {
+        g_error = "out of host memory";
+        return GHX_ERR_NOMEM;
+    }
+    catch (const std::exception& e)
+    {
+        g_error = e.what();
+        return GHX_ERR_PATTERN;
+    }
+}
+
+// Plan cache for the per-field convenience entry points (ghx_structured_pack/unpack): keyed by
+// the bytes of (descriptor, iteration spaces, direction), like the reference's pattern
+// container that outlives its exchanges (include/ghex/pattern_container.hpp:84-87).
+class plan_cache
+{
+    std::mutex mtx_;
+    std::list<std::string> lru_;
+    std::unordered_map<std::string, std::pair<std::unique_ptr<splan>, std::list<std::string>::iterator>> map_;
+    static constexpr size_t kCap = 256;
+
+  public:
+    const splan* get(const ghx_field_desc& f, const ghx_box* boxes, int n, int dir)
+    {
+        std::string key(reinterpret_cast<const char*>(&f), sizeof(f));
+        key.append(reinterpret_cast<const char*>(boxes), sizeof(ghx_box) * size_t(n));
+        key.push_back(char(dir));
+        std::lock_guard<std::mutex> lk(mtx_);
+        auto it = map_.find(key);
+        if (it != map_.end())
+        {
+            lru_.splice(lru_.begin(), lru_, it->second.second);
+            return it->second.first.get();
+        }
+        ghx_pack_entry e{};
+        e.field = f;
+        e.field_slot = 0;
+        e.buffer_slot = 0;
+        e.buffer_offset = 0;
+        e.boxes = boxes;
+        e.n_boxes = n;
+        auto p = std::make_unique<splan>(&e, 1, dir);
+        if (map_.size() >= kCap)
+        {
+            // plans of evicted keys may still be in flight on some stream: drain before freeing
+            (void)hipDeviceSynchronize();
+            map_.erase(lru_.back());
+            lru_.pop_back();
+        }
+        lru_.push_front(key);
+        const splan* raw = p.get();
+        map_.emplace(key, std::make_pair(std::move(p), lru_.begin()));
+        return raw;
+    }
+};
+plan_cache& cache()
+{
+    static plan_cache c;
+    return c;
+}
+}  // namespace
+
+void set_error(const std::string& msg) { g_error = msg; }
+const char* get_error() { return g_error.c_str(); }
+
+// ---------------------------------------------------------------------------------------------
+// exchange planner
+// ---------------------------------------------------------------------------------------------
+struct xbuffer
+{
+    int32_t first_id, second_id, rank, tag;
+    uint64_t size = 0;
+};
+
+struct exchange_plan
+{
+    std::vector<xbuffer> send, recv;
+    std::unique_ptr<splan> spack, sunpack;
+    std::unique_ptr<uplan> upack, uunpack;
+    int32_t n_items = 0;
+};
+}  // namespace ghx
+
+struct ghx_exchange : ghx::exchange_plan
+{
+};
+
+using namespace ghx;
+
+namespace
+{
+// communication_object::allocate (include/ghex/communication_object.hpp:1019-1066)
+void plan_direction(const ghx_exchange_item* items, int n_items, bool receive,
+                    std::vector<xbuffer>& bufs_out, std::vector<ghx_pack_entry>& sent,
+                    std::vector<ghx_upack_entry>& uent, std::vector<std::vector<ghx_box>>& box_store)
+{
+    struct finfo
+    {
+        int item;
+        const halo_entry* e;
+        uint64_t offset;
+    };
+    struct buf
+    {
+        xbuffer x;
+        std::vector<finfo> fields;
+    };
+    std::map<std::pair<int32_t, int32_t>, buf> mem;  // domain_id_pair ordering (:165-174)
+    for (int k = 0; k < n_items; ++k)
+    {
+        const auto& it = items[k];
+        if (!it.pattern) throw invalid("exchange item without pattern");
+        const auto& ps = *it.pattern;
+        if (it.local_index < 0 || it.local_index >= int(ps.doms.size()))
+            throw invalid("exchange item local_index out of range");
+        if ((it.kind == 0) != (ps.kind == 0)) throw invalid("field kind does not match pattern kind");
+        if (it.align < 1 || (it.align & (it.align - 1))) throw invalid("align must be a power of two");
+        const auto& dp = ps.doms[size_t(it.local_index)];
+        const auto& halos = receive ? dp.recv : dp.send;
+        int64_t nc, elem;
+        if (it.kind == 0)
+        {
+            validate_field(it.field);
+            nc = it.field.num_components;
+            elem = it.field.elem_size;
+        }
+        else
+        {
+            nc = it.udata.levels;
+            elem = it.udata.elem_size;
+        }
+        for (const auto& e : halos)
+        {
+            int64_t n = 0;
+            if (it.kind == 0)
+                for (const auto& b : e.boxes) n += b.size(ps.dim);
+            else n = int64_t(e.lids.size());
+            n *= nc;
+            if (n < 1) continue;
+            const auto pair = receive ? std::make_pair(dp.id, e.key.remote_id)
+                                      : std::make_pair(e.key.remote_id, dp.id);
+            auto bi = mem.find(pair);
+            if (bi == mem.end())
+            {
+                buf b;
+                b.x = {pair.first, pair.second, e.key.remote_rank, e.key.tag + it.tag_offset, 0};
+                bi = mem.emplace(pair, std::move(b)).first;
+            }
+            const uint64_t prev = bi->second.x.size;
+            const uint64_t a = uint64_t(it.align);
+            const uint64_t pad = ((prev + a - 1) / a) * a - prev;
+            bi->second.fields.push_back({k, &e, prev + pad});
+            bi->second.x.size += pad + uint64_t(n) * uint64_t(elem);
+        }
+    }
+    int32_t slot = 0;
+    for (auto& kv : mem)
+    {
+        bufs_out.push_back(kv.second.x);
+        for (const auto& fi : kv.second.fields)
+        {
+            const auto& it = items[fi.item];
+            if (it.kind == 0)
+            {
+                const int dim = it.pattern->dim;
+                box_store.emplace_back();
+                auto& bx = box_store.back();
+                for (const auto& b : fi.e->boxes)
+                {
+                    ghx_box g{};
+                    for (int d = 0; d < dim; ++d)
+                    {
+                        g.first[d] = b.lf[d];
+                        g.last[d] = b.ll[d];
+                    }
+                    bx.push_back(g);
+                }
+                if (it.field.dim - (it.field.has_components ? 1 : 0) != dim)
+                    throw invalid("field spatial dimension does not match the pattern");
+                ghx_pack_entry pe{};
+                pe.field = it.field;
+                pe.field_slot = fi.item;
+                pe.buffer_slot = slot;
+                pe.buffer_offset = fi.offset;
+                pe.boxes = bx.data();
+                pe.n_boxes = int32_t(bx.size());
+                sent.push_back(pe);
+            }
+            else
+            {
+                ghx_upack_entry ue{};
+                ue.data = it.udata;
+                ue.field_slot = fi.item;
+                ue.buffer_slot = slot;
+                ue.buffer_offset = fi.offset;
+                ue.lids = fi.e->lids.data();
+                ue.n_lids = int64_t(fi.e->lids.size());
+                uent.push_back(ue);
+            }
+        }
+        ++slot;
+    }
+}
+
+int check_ptr(const void* p, const char* what)
+{
+    if (!p) throw invalid(std::string("null argument: ") + what);
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+const char* ghx_last_error(void) { return ghx::get_error(); }
+
+const char* ghx_version(void) { return "ghex_amd 0.1.0 (gfx950)"; }
+
+int ghx_plan_create(const ghx_pack_entry* entries, int32_t n_entries, int32_t direction,
+                    ghx_plan** out)
+{
+    return guarded([&] {
+        check_ptr(out, "out");
+        if (n_entries < 0 || (n_entries > 0 && !entries)) throw invalid("bad entries");
+        *out = new ghx_plan(entries, n_entries, direction);
+        return GHX_OK;
+    });
+}
+
+int ghx_plan_execute(const ghx_plan* plan, void* const* field_ptrs, int32_t n_field_ptrs,
+                     void* const* buffer_ptrs, int32_t n_buffer_ptrs, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(plan, "plan");
+        return plan->execute(field_ptrs, n_field_ptrs, buffer_ptrs, n_buffer_ptrs, stream);
+    });
+}
+
+int ghx_plan_destroy(ghx_plan* plan)
+{
+    return guarded([&] {
+        delete plan;
+        return GHX_OK;
+    });
+}
+
+int ghx_plan_info(const ghx_plan* plan, uint64_t* bytes, int32_t* n_segments, int32_t* n_tiles)
+{
+    return guarded([&] {
+        check_ptr(plan, "plan");
+        if (bytes) *bytes = plan->bytes;
+        if (n_segments) *n_segments = plan->n_segments;
+        if (n_tiles) *n_tiles = int32_t(plan->n_tiles);
+        return GHX_OK;
+    });
+}
+
+int ghx_structured_pack(const ghx_field_desc* field, const void* field_data, void* buffer,
+                        const ghx_box* boxes, int32_t n_boxes, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(field, "field");
+        if (n_boxes < 0 || (n_boxes > 0 && !boxes)) throw invalid("bad boxes");
+        const splan* p = cache().get(*field, boxes, n_boxes, 0);
+        void* f[1] = {const_cast<void*>(field_data)};
+        void* b[1] = {buffer};
+        return p->execute(f, 1, b, 1, stream);
+    });
+}
+
+int ghx_structured_unpack(const ghx_field_desc* field, void* field_data, const void* buffer,
+                          const ghx_box* boxes, int32_t n_boxes, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(field, "field");
+        if (n_boxes < 0 || (n_boxes > 0 && !boxes)) throw invalid("bad boxes");
+        const splan* p = cache().get(*field, boxes, n_boxes, 1);
+        void* f[1] = {field_data};
+        void* b[1] = {const_cast<void*>(buffer)};
+        return p->execute(f, 1, b, 1, stream);
+    });
+}
+
+int ghx_uplan_create(const ghx_upack_entry* entries, int32_t n_entries, int32_t direction,
+                     ghx_uplan** out)
+{
+    return guarded([&] {
+        check_ptr(out, "out");
+        if (n_entries < 0 || (n_entries > 0 && !entries)) throw invalid("bad entries");
+        *out = new ghx_uplan(entries, n_entries, direction);
+        return GHX_OK;
+    });
+}
+
+int ghx_uplan_execute(const ghx_uplan* plan, void* const* field_ptrs, int32_t n_field_ptrs,
+                      void* const* buffer_ptrs, int32_t n_buffer_ptrs, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(plan, "plan");
+        return plan->execute(field_ptrs, n_field_ptrs, buffer_ptrs, n_buffer_ptrs, stream);
+    });
+}
+
+int ghx_uplan_destroy(ghx_uplan* plan)
+{
+    return guarded([&] {
+        delete plan;
+        return GHX_OK;
+    });
+}
+
+int ghx_uplan_info(const ghx_uplan* plan, uint64_t* bytes, int32_t* n_segments, int32_t* n_tiles)
+{
+    return guarded([&] {
+        check_ptr(plan, "plan");
+        if (bytes) *bytes = plan->bytes;
+        if (n_segments) *n_segments = plan->n_segments;
+        if (n_tiles) *n_tiles = int32_t(plan->n_tiles);
+        return GHX_OK;
+    });
+}
+
+// ----------------------------------------------------------------------------------- patterns
+int ghx_regular_halo_boxes(int32_t dim, const int32_t* global_first, const int32_t* global_last,
+                           const int32_t* halos, const int32_t* periodic,
+                           const int32_t* domain_first, const int32_t* domain_last,
+                           ghx_box* local, ghx_box* global, int32_t max_boxes, int32_t* n_boxes)
+{
+    return guarded([&] {
+        if (dim < 1 || dim > 3) throw invalid("dim must be 1, 2 or 3");
+        check_ptr(global_first, "global_first");
+        check_ptr(global_last, "global_last");
+        check_ptr(halos, "halos");
+        check_ptr(periodic, "periodic");
+        check_ptr(domain_first, "domain_first");
+        check_ptr(domain_last, "domain_last");
+        check_ptr(n_boxes, "n_boxes");
+        auto b = regular_halo_boxes(dim, global_first, global_last, halos, periodic, domain_first,
+                                    domain_last);
+        *n_boxes = int32_t(b.size());
+        for (int32_t i = 0; i < std::min<int32_t>(max_boxes, int32_t(b.size())); ++i)
+        {
+            ghx_box l{}, g{};
+            for (int d = 0; d < dim; ++d)
+            {
+                l.first[d] = b[i].lf[d];
+                l.last[d] = b[i].ll[d];
+                g.first[d] = b[i].gf[d];
+                g.last[d] = b[i].gl[d];
+            }
+            if (local) local[i] = l;
+            if (global) global[i] = g;
+        }
+        return GHX_OK;
+    });
+}
+
+int ghx_regular_pattern_create(int32_t dim, const ghx_regular_domain* domains,
+                               int32_t n_domains, const int32_t* global_first,
+                               const int32_t* global_last, const int32_t* halos,
+                               const int32_t* periodic, int32_t my_rank, ghx_pattern** out)
+{
+    return guarded([&] {
+        check_ptr(out, "out");
+        check_ptr(domains, "domains");
+        check_ptr(global_first, "global_first");
+        check_ptr(global_last, "global_last");
+        check_ptr(halos, "halos");
+        check_ptr(periodic, "periodic");
+        if (dim < 1 || dim > 3) throw invalid("dim must be 1, 2 or 3");
+        if (n_domains < 1) throw invalid("need at least one domain");
+        for (int i = 0; i < n_domains; ++i)
+            for (int j = 0; j < i; ++j)
+                if (domains[i].id == domains[j].id) throw invalid("domain ids must be unique");
+        auto p = std::make_unique<ghx_pattern>();
+        regular_make_pattern(dim, domains, n_domains, global_first, global_last, halos, periodic,
+                             my_rank, *p);
+        *out = p.release();
+        return GHX_OK;
+    });
+}
+
+int ghx_unstructured_pattern_create(int32_t n_domains, const int32_t* domain_ids,
+                                    const int32_t* domain_ranks, const int64_t* gids,
+                                    const int64_t* gid_counts, const int64_t* outer_lids,
+                                    const int64_t* outer_counts, const int64_t* halo_gids,
+                                    const int64_t* halo_counts, int32_t my_rank,
+                                    ghx_pattern** out)
+{
+    return guarded([&] {
+        check_ptr(out, "out");
+        check_ptr(domain_ids, "domain_ids");
+        check_ptr(domain_ranks, "domain_ranks");
+        check_ptr(gid_counts, "gid_counts");
+        check_ptr(outer_counts, "outer_counts");
+        if (n_domains < 1) throw invalid("need at least one domain");
+        auto p = std::make_unique<ghx_pattern>();
+        unstructured_make_pattern(n_domains, domain_ids, domain_ranks, gids, gid_counts,
+                                  outer_lids, outer_counts, halo_gids, halo_counts, my_rank, *p);
+        *out = p.release();
+        return GHX_OK;
+    });
+}
+
+int ghx_pattern_destroy(ghx_pattern* p)
+{
+    return guarded([&] {
+        delete p;
+        return GHX_OK;
+    });
+}
+
+int ghx_pattern_num_domains(const ghx_pattern* p, int32_t* n)
+{
+    return guarded([&] {
+        check_ptr(p, "pattern");
+        check_ptr(n, "n");
+        *n = int32_t(p->doms.size());
+        return GHX_OK;
+    });
+}
+
+int ghx_pattern_max_tag(const ghx_pattern* p, int32_t* max_tag)
+{
+    return guarded([&] {
+        check_ptr(p, "pattern");
+        check_ptr(max_tag, "max_tag");
+        *max_tag = p->max_tag;
+        return GHX_OK;
+    });
+}
+
+int ghx_pattern_domain_id(const ghx_pattern* p, int32_t local_index, int32_t* id)
+{
+    return guarded([&] {
+        check_ptr(p, "pattern");
+        check_ptr(id, "id");
+        if (local_index < 0 || local_index >= int32_t(p->doms.size())) throw invalid("local_index");
+        *id = p->doms[size_t(local_index)].id;
+        return GHX_OK;
+    });
+}
+
+static const ghx::halo_entry& key_of(const ghx_pattern* p, int32_t li, int32_t dir, int32_t key)
+{
+    if (!p) throw invalid("null pattern");
+    if (li < 0 || li >= int32_t(p->doms.size())) throw invalid("local_index out of range");
+    const auto& v = dir == 0 ? p->doms[size_t(li)].send : p->doms[size_t(li)].recv;
+    if (key < 0 || key >= int32_t(v.size())) throw invalid("key out of range");
+    return v[size_t(key)];
+}
+
+int ghx_pattern_num_keys(const ghx_pattern* p, int32_t local_index, int32_t direction,
+                         int32_t* n_keys)
+{
+    return guarded([&] {
+        check_ptr(p, "pattern");
+        check_ptr(n_keys, "n_keys");
+        if (local_index < 0 || local_index >= int32_t(p->doms.size())) throw invalid("local_index");
+        const auto& d = p->doms[size_t(local_index)];
+        *n_keys = int32_t(direction == 0 ? d.send.size() : d.recv.size());
+        return GHX_OK;
+    });
+}
+
+int ghx_pattern_key(const ghx_pattern* p, int32_t local_index, int32_t direction, int32_t key,
+                    int32_t* remote_id, int32_t* remote_rank, int32_t* tag, int32_t* n_spaces,
+                    int64_t* n_elements)
+{
+    return guarded([&] {
+        const auto& e = key_of(p, local_index, direction, key);
+        if (remote_id) *remote_id = e.key.remote_id;
+        if (remote_rank) *remote_rank = e.key.remote_rank;
+        if (tag) *tag = e.key.tag;
+        if (p->kind == 0)
+        {
+            if (n_spaces) *n_spaces = int32_t(e.boxes.size());
+            if (n_elements)
+            {
+                int64_t n = 0;
+                for (const auto& b : e.boxes) n += b.size(p->dim);
+                *n_elements = n;
+            }
+        }
+        else
+        {
+            if (n_spaces) *n_spaces = 1;
+            if (n_elements) *n_elements = int64_t(e.lids.size());
+        }
+        return GHX_OK;
+    });
+}
+
+int ghx_pattern_key_boxes(const ghx_pattern* p, int32_t local_index, int32_t direction,
+                          int32_t key, ghx_box* local, ghx_box* global, int32_t max_boxes)
+{
+    return guarded([&] {
+        const auto& e = key_of(p, local_index, direction, key);
+        if (p->kind != 0) throw invalid("not a structured pattern");
+        for (int32_t i = 0; i < std::min<int32_t>(max_boxes, int32_t(e.boxes.size())); ++i)
+        {
+            ghx_box l{}, g{};
+            for (int d = 0; d < p->dim; ++d)
+            {
+                l.first[d] = e.boxes[size_t(i)].lf[d];
+                l.last[d] = e.boxes[size_t(i)].ll[d];
+                g.first[d] = e.boxes[size_t(i)].gf[d];
+                g.last[d] = e.boxes[size_t(i)].gl[d];
+            }
+            if (local) local[i] = l;
+            if (global) global[i] = g;
+        }
+        return GHX_OK;
+    });
+}
+
+int ghx_pattern_key_lids(const ghx_pattern* p, int32_t local_index, int32_t direction,
+                         int32_t key, int64_t* lids, int64_t max_lids)
+{
+    return guarded([&] {
+        const auto& e = key_of(p, local_index, direction, key);
+        if (p->kind != 1) throw invalid("not an unstructured pattern");
+        check_ptr(lids, "lids");
+        const int64_t n = std::min<int64_t>(max_lids, int64_t(e.lids.size()));
+        std::memcpy(lids, e.lids.data(), size_t(n) * sizeof(int64_t));
+        return GHX_OK;
+    });
+}
+
+// ---------------------------------------------------------------------------------- exchange
+int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exchange** out)
+{
+    return guarded([&] {
+        check_ptr(out, "out");
+        if (n_items < 1 || !items) throw invalid("need at least one exchange item");
+        if (n_items > GHX_MAX_SLOTS) throw invalid("at most 64 fields per exchange");
+        auto ex = std::make_unique<ghx_exchange>();
+        ex->n_items = n_items;
+        for (int dir = 0; dir < 2; ++dir)
+        {
+            const bool receive = dir == 1;
+            std::vector<ghx_pack_entry> sent;
+            std::vector<ghx_upack_entry> uent;
+            std::vector<std::vector<ghx_box>> store;
+            store.reserve(size_t(n_items) * 64);
+            auto& bufs = receive ? ex->recv : ex->send;
+            plan_direction(items, n_items, receive, bufs, sent, uent, store);
+            if (bufs.size() > GHX_MAX_SLOTS) throw invalid("more than 64 peer buffers");
+            if (!sent.empty())
+                (receive ? ex->sunpack : ex->spack) =
+                    std::make_unique<splan>(sent.data(), int(sent.size()), receive ? 1 : 0);
+            if (!uent.empty())
+                (receive ? ex->uunpack : ex->upack) =
+                    std::make_unique<uplan>(uent.data(), int(uent.size()), receive ? 1 : 0);
+        }
+        *out = ex.release();
+        return GHX_OK;
+    });
+}
+
+int ghx_exchange_destroy(ghx_exchange* ex)
+{
+    return guarded([&] {
+        delete ex;
+        return GHX_OK;
+    });
+}
+
+int ghx_exchange_num_buffers(const ghx_exchange* ex, int32_t direction, int32_t* n)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        check_ptr(n, "n");
+        *n = int32_t(direction == 0 ? ex->send.size() : ex->recv.size());
+        return GHX_OK;
+    });
+}
+
+int ghx_exchange_buffer(const ghx_exchange* ex, int32_t direction, int32_t index,
+                        int32_t* first_id, int32_t* second_id, int32_t* rank, int32_t* tag,
+                        uint64_t* size)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        const auto& v = direction == 0 ? ex->send : ex->recv;
+        if (index < 0 || index >= int32_t(v.size())) throw invalid("buffer index out of range");
+        const auto& b = v[size_t(index)];
+        if (first_id) *first_id = b.first_id;
+        if (second_id) *second_id = b.second_id;
+        if (rank) *rank = b.rank;
+        if (tag) *tag = b.tag;
+        if (size) *size = b.size;
+        return GHX_OK;
+    });
+}
+
+int ghx_exchange_pack(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                      void* const* send_buffers, int32_t n_send, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        if (n_send < int32_t(ex->send.size())) throw invalid("too few send buffers");
+        int rc = GHX_OK;
+        if (ex->spack) rc = ex->spack->execute(field_ptrs, n_fields, send_buffers, n_send, stream);
+        if (rc == GHX_OK && ex->upack)
+            rc = ex->upack->execute(field_ptrs, n_fields, send_buffers, n_send, stream);
+        return rc;
+    });
+}
+
+int ghx_exchange_unpack(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                        void* const* recv_buffers, int32_t n_recv, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        if (n_recv < int32_t(ex->recv.size())) throw invalid("too few recv buffers");
+        int rc = GHX_OK;
+        if (ex->sunpack) rc = ex->sunpack->execute(field_ptrs, n_fields, recv_buffers, n_recv, stream);
+        if (rc == GHX_OK && ex->uunpack)
+            rc = ex->uunpack->execute(field_ptrs, n_fields, recv_buffers, n_recv, stream);
+        return rc;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,111 @@
+// ghx_internal.hpp — structures shared by the host planner and the gfx950 kernels.
+//
+// Data layout in HBM: a plan is a flat table of segments (one per field x
+// iteration space) plus a tile table (uint32 segment index per workgroup tile). A segment is a
+// set of equal-length contiguous byte runs ("rows") of the field that map, in order, onto ONE
+// contiguous byte range of the buffer — the dense buffer box of make_buffer_desc
+// (include/ghex/structured/regular/field_descriptor.hpp:114-129) is row-major in the field's
+// layout order, so row r occupies buffer bytes [r*L, (r+1)*L). Rows are decoded from the
+// buffer byte position by magic-number division (no hardware divide on the hot path).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/ghx.h"
+
+namespace ghx
+{
+// Bytes of buffer covered by one workgroup tile (256 threads x 4 vectors x 16 B).
+constexpr uint32_t kTileBytes = 16384;
+constexpr int kBlock = 256;
+
+// Unsigned 32-bit division by an invariant d via multiply-high (Granlund-Montgomery; the
+// round-up variant valid for every n < 2^32): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(m, n).
+struct magic_u32
+{
+    uint32_t m;
+    uint8_t s1, s2;
+    uint16_t pad;
+};
+
+inline magic_u32 make_magic(uint32_t d)
+{
+    magic_u32 r{};
+    if (d == 0) d = 1;
+    int l = 0;
+    while ((uint64_t(1) << l) < d) ++l;  // l = ceil(log2 d)
+    uint64_t m = ((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1;
+    r.m = uint32_t(m);
+    r.s1 = uint8_t(l < 1 ? l : 1);
+    r.s2 = uint8_t(l > 1 ? l - 1 : 0);
+    return r;
+}
+
+// Structured segment (128 B, read once per workgroup tile with scalar loads).
+struct alignas(16) seg_s
+{
+    int64_t field_off;    // byte offset (from the field base) of the segment's first row
+    uint64_t buf_off;     // byte offset (from the buffer base) of the segment's first byte
+    int64_t stride[4];    // field byte stride of outer dim k (k = 0 varies fastest over rows)
+    uint32_t ext[4];      // outer extents (1 for unused dims)
+    magic_u32 mag_row;    // division by row_bytes
+    magic_u32 mag_ext[3]; // division by ext[0], ext[1], ext[2]
+    uint32_t row_bytes;   // L: bytes per contiguous run
+    uint32_t bytes;       // rows * L
+    uint32_t first_tile;  // first tile index of this segment
+    uint16_t field_slot;
+    uint16_t buf_slot;
+    uint8_t wlog2;        // log2 of the widest vector (<= 16 B) that divides L, offsets, strides
+    uint8_t n_outer;
+    uint8_t pad[14];
+};
+static_assert(sizeof(seg_s) == 128, "seg_s layout");
+
+// Unstructured segment: rows come from an index list.
+struct alignas(16) seg_u
+{
+    uint64_t buf_off;
+    const void* lids;          // device array, int32 or int64
+    int64_t index_stride_b;    // bytes
+    int64_t level_stride_b;    // bytes
+    magic_u32 mag_row;         // division by row_bytes
+    magic_u32 mag_inner;       // levels_first: division by levels_per_row-group; else by n
+    uint32_t n;                // number of indices
+    uint32_t row_levels;       // levels per row group when rows are per (i,l); see planner
+    uint32_t row_bytes;
+    uint32_t bytes;
+    uint32_t first_tile;
+    uint16_t field_slot;
+    uint16_t buf_slot;
+    uint8_t wlog2;
+    uint8_t mode;              // 0: row = index i (levels contiguous, L = levels*elem)
+                               // 1: rows (i,l) i-major (levels_first, strided levels)
+                               // 2: rows (l,i) l-major (levels_last)
+    uint8_t lid64;
+    uint8_t pad[13];
+};
+static_assert(sizeof(seg_u) == 96, "seg_u layout");
+
+// Kernel arguments (passed by value: <= 1.1 KB of kernarg).
+struct kargs
+{
+    const void* segs;
+    const uint32_t* tile_seg;
+    uint32_t n_tiles;
+    uint32_t pad;
+    uint64_t field_ptr[GHX_MAX_SLOTS];
+    uint64_t buf_ptr[GHX_MAX_SLOTS];
+};
+
+// thread-local last error
+void set_error(const std::string& msg);
+const char* get_error();
+
+// kernel launchers (ghx_kernels.hip)
+int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid);
+int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid);
+uint32_t grid_for_tiles(uint32_t n_tiles);
+
+}  // namespace ghx

@@ -1,0 +1,276 @@
+// ghx_kernels.hip — gfx950 (CDNA4) pack / unpack kernels for the halo path.
+//
+// One launch covers every (field, iteration space, buffer) of a plan. Work is cut in the
+// BUFFER's byte space: a workgroup tile is kTileBytes (16 KiB) of one segment's buffer range,
+// so the buffer side is always a linear, fully coalesced 16 B/lane stream, and the field side
+// is linear within each contiguous row. Each lane decodes its buffer byte position into
+// (row, column) and the row into field coordinates with magic-number division, so no launch
+// depends on the shape of an iteration space: face, edge and corner spaces of all fields share
+// the one grid (the reference launches one kernel per iteration space per field,
+// include/ghex/structured/pack_kernels.hpp:216-241, with a per-element 32-bit divide chain,
+// include/ghex/structured/field_utils.hpp:128-159).
+//
+// Vector width per segment: the widest W in {16,8,4,2,1} bytes dividing the row length, the
+// row offsets/strides (planner) and the runtime base pointers (checked per tile here), so the
+// same plan is correct for any pointer alignment. No MFMA: this path is pure data movement.
+#include <hip/hip_runtime.h>
+
+#include "ghx_internal.hpp"
+
+namespace ghx
+{
+namespace
+{
+__device__ __forceinline__ uint32_t fastdiv(uint32_t n, magic_u32 m)
+{
+    const uint32_t t = __umulhi(m.m, n);
+    return (t + ((n - t) >> m.s1)) >> m.s2;
+}
+
+template<int W>
+struct vec_t;
+template<>
+struct vec_t<16>
+{
+    using type = uint4;
+};
+template<>
+struct vec_t<8>
+{
+    using type = uint2;
+};
+template<>
+struct vec_t<4>
+{
+    using type = uint32_t;
+};
+template<>
+struct vec_t<2>
+{
+    using type = uint16_t;
+};
+template<>
+struct vec_t<1>
+{
+    using type = uint8_t;
+};
+
+constexpr int kUnroll = 4;
+
+// field byte offset of segment-relative buffer position p (structured)
+__device__ __forceinline__ int64_t field_offset_s(const seg_s& s, uint32_t p)
+{
+    const uint32_t row = fastdiv(p, s.mag_row);
+    const uint32_t col = p - row * s.row_bytes;
+    const uint32_t q0 = fastdiv(row, s.mag_ext[0]);
+    const uint32_t c0 = row - q0 * s.ext[0];
+    const uint32_t q1 = fastdiv(q0, s.mag_ext[1]);
+    const uint32_t c1 = q0 - q1 * s.ext[1];
+    const uint32_t q2 = fastdiv(q1, s.mag_ext[2]);
+    const uint32_t c2 = q1 - q2 * s.ext[2];
+    return s.field_off + int64_t(c0) * s.stride[0] + int64_t(c1) * s.stride[1] +
+           int64_t(c2) * s.stride[2] + int64_t(q2) * s.stride[3] + int64_t(col);
+}
+
+template<bool PACK, int W>
+__device__ __forceinline__ void copy_tile_s(const seg_s& s, char* __restrict__ field,
+                                            char* __restrict__ buf, uint32_t start, uint32_t end)
+{
+    using V = typename vec_t<W>::type;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t base = start + tid * W; base < end; base += kUnroll * kBlock * W)
+    {
+        V v[kUnroll];
+        int64_t fo[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                fo[u] = field_offset_s(s, p);
+                if (PACK) v[u] = *reinterpret_cast<const V*>(field + fo[u]);
+                else v[u] = *reinterpret_cast<const V*>(buf + p);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                if (PACK) *reinterpret_cast<V*>(buf + p) = v[u];
+                else *reinterpret_cast<V*>(field + fo[u]) = v[u];
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int ptr_wlog2(uint64_t p)
+{
+    // log2 of the largest power of two (<= 16) dividing p
+    return __builtin_ctzll(p | 16ull);
+}
+
+template<bool PACK>
+__global__ __launch_bounds__(kBlock) void k_structured(kargs a)
+{
+    const seg_s* __restrict__ segs = static_cast<const seg_s*>(a.segs);
+    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
+    {
+        const uint32_t si = a.tile_seg[t];
+        const seg_s s = segs[si];
+        const uint32_t start = (t - s.first_tile) * kTileBytes;
+        const uint32_t end = min(start + kTileBytes, s.bytes);
+        char* field = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
+        char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
+        int w = s.wlog2;
+        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
+        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+        switch (w)
+        {
+            case 4: copy_tile_s<PACK, 16>(s, field, buf, start, end); break;
+            case 3: copy_tile_s<PACK, 8>(s, field, buf, start, end); break;
+            case 2: copy_tile_s<PACK, 4>(s, field, buf, start, end); break;
+            case 1: copy_tile_s<PACK, 2>(s, field, buf, start, end); break;
+            default: copy_tile_s<PACK, 1>(s, field, buf, start, end); break;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// unstructured: rows come from an index list
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t load_lid(const seg_u& s, uint32_t i)
+{
+    if (s.lid64) return static_cast<const int64_t*>(s.lids)[i];
+    return static_cast<const int32_t*>(s.lids)[i];
+}
+
+__device__ __forceinline__ int64_t field_offset_u(const seg_u& s, uint32_t p)
+{
+    const uint32_t row = fastdiv(p, s.mag_row);
+    const uint32_t col = p - row * s.row_bytes;
+    uint32_t i, l;
+    if (s.mode == 0)
+    {
+        i = row;
+        l = 0;
+    }
+    else if (s.mode == 1)
+    {
+        i = fastdiv(row, s.mag_inner);
+        l = row - i * s.row_levels;
+    }
+    else
+    {
+        l = fastdiv(row, s.mag_inner);
+        i = row - l * s.n;
+    }
+    return load_lid(s, i) * s.index_stride_b + int64_t(l) * s.level_stride_b + int64_t(col);
+}
+
+template<bool PACK, int W>
+__device__ __forceinline__ void copy_tile_u(const seg_u& s, char* __restrict__ field,
+                                            char* __restrict__ buf, uint32_t start, uint32_t end)
+{
+    using V = typename vec_t<W>::type;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t base = start + tid * W; base < end; base += kUnroll * kBlock * W)
+    {
+        V v[kUnroll];
+        int64_t fo[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end) fo[u] = field_offset_u(s, p);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                if (PACK) v[u] = *reinterpret_cast<const V*>(field + fo[u]);
+                else v[u] = *reinterpret_cast<const V*>(buf + p);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                if (PACK) *reinterpret_cast<V*>(buf + p) = v[u];
+                else *reinterpret_cast<V*>(field + fo[u]) = v[u];
+            }
+        }
+    }
+}
+
+template<bool PACK>
+__global__ __launch_bounds__(kBlock) void k_unstructured(kargs a)
+{
+    const seg_u* __restrict__ segs = static_cast<const seg_u*>(a.segs);
+    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
+    {
+        const uint32_t si = a.tile_seg[t];
+        const seg_u s = segs[si];
+        const uint32_t start = (t - s.first_tile) * kTileBytes;
+        const uint32_t end = min(start + kTileBytes, s.bytes);
+        char* field = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
+        char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
+        int w = s.wlog2;
+        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
+        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+        switch (w)
+        {
+            case 4: copy_tile_u<PACK, 16>(s, field, buf, start, end); break;
+            case 3: copy_tile_u<PACK, 8>(s, field, buf, start, end); break;
+            case 2: copy_tile_u<PACK, 4>(s, field, buf, start, end); break;
+            case 1: copy_tile_u<PACK, 2>(s, field, buf, start, end); break;
+            default: copy_tile_u<PACK, 1>(s, field, buf, start, end); break;
+        }
+    }
+}
+}  // namespace
+
+uint32_t grid_for_tiles(uint32_t n_tiles)
+{
+    // one tile per workgroup (hardware dispatch balances); grid-stride beyond 1M tiles
+    return n_tiles < (1u << 20) ? n_tiles : (1u << 20);
+}
+
+int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid)
+{
+    if (a.n_tiles == 0) return GHX_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (direction == 0) hipLaunchKernelGGL(k_structured<true>, dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_structured<false>, dim3(grid), dim3(kBlock), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+    {
+        set_error(std::string("structured kernel launch failed: ") + hipGetErrorString(e));
+        return GHX_ERR_HIP;
+    }
+    return GHX_OK;
+}
+
+int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid)
+{
+    if (a.n_tiles == 0) return GHX_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (direction == 0)
+        hipLaunchKernelGGL(k_unstructured<true>, dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_unstructured<false>, dim3(grid), dim3(kBlock), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+    {
+        set_error(std::string("unstructured kernel launch failed: ") + hipGetErrorString(e));
+        return GHX_ERR_HIP;
+    }
+    return GHX_OK;
+}
+
+}  // namespace ghx

@@ -1,0 +1,348 @@
+// ghx_pattern.cpp — structured and unstructured halo patterns, computed on the host.
+//
+// The pattern fixes the packed byte layout (its iteration-space order is the buffer order), so
+// these follow the reference's ordering rules exactly. Setup collectives are replaced by taking
+// every rank's domains as input (the caller all-gathers them once, e.g. with torch.distributed),
+// after which each rank derives its own maps locally with no further communication.
+#include "ghx_pattern.hpp"
+
+#include <algorithm>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+
+namespace ghx
+{
+// ---------------------------------------------------------------------------------------------
+// structured, regular
+// ---------------------------------------------------------------------------------------------
+std::vector<is_pair> regular_halo_boxes(int dim, const int32_t* gfirst, const int32_t* glast,
+                                        const int32_t* halos, const int32_t* periodic,
+                                        const int32_t* dfirst, const int32_t* dlast)
+{
+    // the three 1-D spaces {left, middle, right} per dimension (halo_generator.hpp:95-118)
+    int32_t sp[3][3][4];  // [space][dim][lf, ll, gf, gl]
+    for (int d = 0; d < dim; ++d)
+    {
+        const int32_t lf = -halos[2 * d];
+        sp[0][d][0] = lf;
+        sp[0][d][1] = -1;
+        sp[0][d][2] = lf + dfirst[d];
+        sp[0][d][3] = dfirst[d] - 1;
+        sp[1][d][0] = 0;
+        sp[1][d][1] = dlast[d] - dfirst[d];
+        sp[1][d][2] = dfirst[d];
+        sp[1][d][3] = dlast[d];
+        sp[2][d][0] = sp[1][d][1] + 1;
+        sp[2][d][1] = sp[1][d][1] + halos[2 * d + 1];
+        sp[2][d][2] = dlast[d] + 1;
+        sp[2][d][3] = dlast[d] + halos[2 * d + 1];
+    }
+    // compute_spaces (:163-197): dimension 0 is the outermost recursion level, i.e. the most
+    // significant base-3 digit; the centre (3^D/2) and empty boxes are dropped (:124-131).
+    int n3 = 1;
+    for (int d = 0; d < dim; ++d) n3 *= 3;
+    std::vector<is_pair> out;
+    for (int j = 0; j < n3; ++j)
+    {
+        if (j == n3 / 2) continue;
+        is_pair b{};
+        int r = j;
+        int digit[3] = {0, 0, 0};
+        for (int d = dim - 1; d >= 0; --d)
+        {
+            digit[d] = r % 3;
+            r /= 3;
+        }
+        bool empty = false;
+        for (int d = 0; d < dim; ++d)
+        {
+            const int32_t* s = sp[digit[d]][d];
+            b.lf[d] = s[0];
+            b.ll[d] = s[1];
+            b.gf[d] = s[2];
+            b.gl[d] = s[3];
+            if (b.ll[d] < b.lf[d]) empty = true;
+        }
+        if (!empty) out.push_back(b);
+    }
+    // periodic wrap of the global coordinates (:133-145)
+    for (auto& b : out)
+        for (int d = 0; d < dim; ++d)
+        {
+            if (!periodic[d]) continue;
+            const int32_t ext_h = b.gl[d] - b.gf[d];
+            const int32_t ext = glast[d] + 1 - gfirst[d];
+            const int32_t off = b.gf[d] - gfirst[d];
+            b.gf[d] = (off + ext) % ext + gfirst[d];
+            b.gl[d] = b.gf[d] + ext_h;
+        }
+    return out;
+}
+
+int regular_make_pattern(int dim, const ghx_regular_domain* doms, int n, const int32_t* gfirst,
+                         const int32_t* glast, const int32_t* halos, const int32_t* periodic,
+                         int my_rank, pattern_set& out)
+{
+    if (dim < 1 || dim > 3 || n < 1) throw std::runtime_error("regular pattern: bad dim / count");
+    // ranks in ascending order, each rank's domains in their given order (pattern.hpp:302-308)
+    int world = 0;
+    for (int i = 0; i < n; ++i) world = std::max(world, doms[i].rank + 1);
+    std::vector<std::vector<int>> by_rank(world);
+    for (int i = 0; i < n; ++i)
+    {
+        if (doms[i].rank < 0) throw std::runtime_error("regular pattern: negative rank");
+        by_rank[doms[i].rank].push_back(i);
+    }
+    // recv halos of every domain (all ranks: the receivers assign the tags that the senders'
+    // keys carry): boxes x ranks x domains, keyed by the remote domain id (pattern.hpp:290-329)
+    struct recv_map
+    {
+        std::map<int32_t, std::pair<int32_t, std::vector<is_pair>>> by_id;  // id -> (rank, IS)
+        std::vector<halo_entry> entries;                                    // with tags
+    };
+    std::vector<recv_map> recv(n);
+    for (int a = 0; a < n; ++a)
+    {
+        const auto& d = doms[a];
+        auto boxes = regular_halo_boxes(dim, gfirst, glast, halos, periodic, d.first, d.last);
+        for (const auto& b : boxes)
+            for (int j = 0; j < world; ++j)
+                for (int k : by_rank[j])
+                {
+                    const auto& o = doms[k];
+                    is_pair x{};
+                    bool ok = true;
+                    for (int c = 0; c < dim; ++c)
+                    {
+                        x.gf[c] = std::max(b.gf[c], o.first[c]);
+                        x.gl[c] = std::min(b.gl[c], o.last[c]);
+                        x.lf[c] = b.lf[c] + (x.gf[c] - b.gf[c]);
+                        x.ll[c] = b.lf[c] + (x.gl[c] - b.gf[c]);
+                        if (x.gf[c] > x.gl[c]) ok = false;
+                    }
+                    if (!ok) continue;
+                    auto it = recv[a].by_id.find(o.id);
+                    if (it == recv[a].by_id.end())
+                        it = recv[a].by_id.emplace(o.id, std::make_pair(o.rank, std::vector<is_pair>{})).first;
+                    it->second.second.push_back(x);
+                }
+    }
+    // tags: per receiving rank, per remote rank 0,1,2,... over its patterns in order, each
+    // pattern's map in key order (pattern.hpp:331-367)
+    int32_t max_tag = 0;
+    for (int r = 0; r < world; ++r)
+    {
+        std::map<int32_t, int32_t> tag_map;
+        for (int a : by_rank[r])
+            for (auto& kv : recv[a].by_id)
+            {
+                const int32_t rr = kv.second.first;
+                int32_t tag;
+                auto it = tag_map.find(rr);
+                if (it == tag_map.end())
+                {
+                    tag_map[rr] = 0;
+                    tag = 0;
+                }
+                else
+                {
+                    tag = ++it->second;
+                    max_tag = std::max(max_tag, tag);
+                }
+                halo_entry e;
+                e.key = {kv.first, rr, tag};
+                e.boxes = kv.second.second;
+                recv[a].entries.push_back(std::move(e));
+            }
+    }
+    // my patterns: recv maps as computed; send maps = the receivers' lists translated into my
+    // local coordinates, keyed (receiver id, tag) (pattern.hpp:369-437, 536-561)
+    out = pattern_set{};
+    out.kind = 0;
+    out.dim = dim;
+    out.max_tag = max_tag;
+    if (my_rank < 0 || my_rank >= world) return GHX_OK;
+    for (int a : by_rank[my_rank])
+    {
+        domain_pattern p;
+        p.id = doms[a].id;
+        p.recv = recv[a].entries;  // already in (id, tag) order: ids unique per map
+        std::map<std::pair<int32_t, int32_t>, halo_entry> send;
+        for (int b = 0; b < n; ++b)
+            for (const auto& e : recv[b].entries)
+            {
+                if (e.key.remote_id != doms[a].id || e.key.remote_rank != my_rank) continue;
+                halo_entry s;
+                s.key = {doms[b].id, doms[b].rank, e.key.tag};
+                for (auto x : e.boxes)
+                {
+                    for (int c = 0; c < dim; ++c)
+                    {
+                        x.lf[c] = x.gf[c] - doms[a].first[c];
+                        x.ll[c] = x.gl[c] - doms[a].first[c];
+                    }
+                    s.boxes.push_back(x);
+                }
+                send.emplace(std::make_pair(s.key.remote_id, s.key.tag), std::move(s));
+            }
+        for (auto& kv : send) p.send.push_back(std::move(kv.second));
+        out.doms.push_back(std::move(p));
+    }
+    return GHX_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// unstructured
+// ---------------------------------------------------------------------------------------------
+namespace
+{
+struct udomain
+{
+    int32_t id, rank;
+    std::vector<int64_t> gids;
+    std::unordered_map<int64_t, int64_t> inner;
+    // unordered_multimap equal_range order of libstdc++: reverse insertion order
+    std::unordered_map<int64_t, std::vector<int64_t>> outer;
+    std::vector<int64_t> outer_gids;
+
+    // domain_descriptor::make_outer_lids (user_concepts.hpp:88-113)
+    std::vector<int64_t> make_outer_lids(const std::vector<int64_t>& g) const
+    {
+        std::vector<int64_t> lids;
+        lids.reserve(g.size());
+        std::unordered_map<int64_t, size_t> count;
+        for (auto gid : g)
+        {
+            auto it = outer.find(gid);
+            if (it == outer.end()) continue;
+            auto c = count.find(gid);
+            if (c == count.end())
+            {
+                count.emplace(gid, 0);
+                lids.push_back(it->second[0]);
+            }
+            else
+            {
+                if (++c->second < it->second.size()) lids.push_back(it->second[c->second]);
+                else throw std::runtime_error("halo gid does not have an associated lid in the domain");
+            }
+        }
+        for (auto& kv : count)
+            if (kv.second + 1 != outer.find(kv.first)->second.size())
+                throw std::runtime_error("halo gid occurs not often enough");
+        return lids;
+    }
+};
+
+unsigned num_bits(unsigned n) { return n ? 1u + num_bits(n >> 1) : 1u; }
+}  // namespace
+
+int unstructured_make_pattern(int n, const int32_t* ids, const int32_t* ranks,
+                              const int64_t* gids, const int64_t* gid_counts,
+                              const int64_t* outer_lids, const int64_t* outer_counts,
+                              const int64_t* halo_gids, const int64_t* halo_counts, int my_rank,
+                              pattern_set& out)
+{
+    // domain_descriptor ctor (user_concepts.hpp:143-175)
+    std::vector<udomain> D(n);
+    int64_t go = 0, oo = 0;
+    for (int i = 0; i < n; ++i)
+    {
+        auto& d = D[i];
+        d.id = ids[i];
+        d.rank = ranks[i];
+        std::unordered_set<int64_t> outer_set;
+        for (int64_t k = 0; k < outer_counts[i]; ++k)
+            if (!outer_set.insert(outer_lids[oo + k]).second)
+                throw std::runtime_error("repeated outer (local) index");
+        oo += outer_counts[i];
+        for (int64_t lid = 0; lid < gid_counts[i]; ++lid)
+        {
+            const int64_t gid = gids[go + lid];
+            if (outer_set.count(lid))
+            {
+                auto& v = d.outer[gid];
+                v.insert(v.begin(), lid);
+                d.outer_gids.push_back(gid);
+            }
+            else if (!d.inner.emplace(gid, lid).second)
+                throw std::runtime_error("repeated inner (global) index");
+            d.gids.push_back(gid);
+        }
+        go += gid_counts[i];
+    }
+    int world = 0;
+    for (auto& d : D) world = std::max(world, d.rank + 1);
+    std::vector<std::vector<int>> by_rank(world);
+    for (int i = 0; i < n; ++i) by_rank[D[i].rank].push_back(i);
+    unsigned max_num_domains = 0;
+    int32_t max_domain_id = 0;
+    for (auto& v : by_rank) max_num_domains = std::max<unsigned>(max_num_domains, v.size());
+    for (auto& d : D) max_domain_id = std::max(max_domain_id, d.id);
+    const unsigned shift = num_bits(max_num_domains);
+    auto make_tag = [shift](unsigned src_local_idx, int32_t tgt) {
+        return int32_t((src_local_idx << shift) | unsigned(tgt));
+    };
+    // halo gids of every domain, in halo (generator) order
+    std::vector<std::vector<int64_t>> halo(n);
+    int64_t ho = 0;
+    for (int i = 0; i < n; ++i)
+    {
+        std::vector<int64_t> hg;
+        if (halo_gids && halo_counts && halo_counts[i] >= 0)
+        {
+            hg.assign(halo_gids + ho, halo_gids + ho + halo_counts[i]);
+            ho += halo_counts[i];
+        }
+        else hg = D[i].outer_gids;
+        for (auto lid : D[i].make_outer_lids(hg)) halo[i].push_back(D[i].gids[lid]);
+    }
+    // send halos of domain s (local index i on its rank) towards every domain o (:272-330);
+    // recv halos = make_outer_lids of the same gid sequence on the receiver (:337-365)
+    out = pattern_set{};
+    out.kind = 1;
+    out.dim = 1;
+    out.max_tag = make_tag(max_num_domains, max_domain_id);
+    if (my_rank >= world) return GHX_OK;
+    for (size_t li = 0; li < by_rank[my_rank].size(); ++li)
+    {
+        const int a = by_rank[my_rank][li];
+        const auto& d = D[a];
+        domain_pattern p;
+        p.id = d.id;
+        std::map<std::pair<int32_t, int32_t>, halo_entry> send, recv;
+        for (int o = 0; o < n; ++o)
+        {
+            halo_entry e;
+            for (auto g : halo[o])
+            {
+                auto it = d.inner.find(g);
+                if (it != d.inner.end()) e.lids.push_back(it->second);
+            }
+            if (e.lids.empty()) continue;
+            e.key = {D[o].id, D[o].rank, make_tag(unsigned(li), D[o].id)};
+            send.emplace(std::make_pair(e.key.remote_rank, e.key.tag), std::move(e));
+        }
+        for (int src = 0; src < world; ++src)
+            for (size_t sj = 0; sj < by_rank[src].size(); ++sj)
+            {
+                const auto& s = D[by_rank[src][sj]];
+                std::vector<int64_t> g;
+                for (auto x : halo[a])
+                    if (s.inner.count(x)) g.push_back(x);
+                if (g.empty()) continue;
+                halo_entry e;
+                e.key = {s.id, s.rank, make_tag(unsigned(sj), d.id)};
+                e.lids = d.make_outer_lids(g);
+                recv.emplace(std::make_pair(e.key.remote_rank, e.key.tag), std::move(e));
+            }
+        for (auto& kv : send) p.send.push_back(std::move(kv.second));
+        for (auto& kv : recv) p.recv.push_back(std::move(kv.second));
+        out.doms.push_back(std::move(p));
+    }
+    return GHX_OK;
+}
+}  // namespace ghx

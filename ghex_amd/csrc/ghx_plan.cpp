@@ -1,0 +1,394 @@
+// ghx_plan.cpp — host-side planner: iteration spaces -> device segment + tile tables.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+#include "ghx_plan.hpp"
+
+namespace ghx
+{
+namespace
+{
+int ctz64(uint64_t v) { return v ? __builtin_ctzll(v) : 64; }
+
+int wlog2_of(uint64_t v)  // log2 of the largest power of two <= 16 dividing v
+{
+    return std::min(4, ctz64(v));
+}
+
+uint32_t tiles_of(uint32_t bytes) { return (bytes + kTileBytes - 1) / kTileBytes; }
+
+bool have_device()
+{
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+// Upload a plan's host tables to device memory (synchronous: plan creation is setup time).
+// Without a HIP device (the CPU build container) the plan stays host-only: its metadata can be
+// inspected, executing it reports GHX_ERR_HIP.
+template<typename Seg>
+void upload(device_tables& dt, const std::vector<Seg>& segs, const std::vector<uint32_t>& tiles)
+{
+    dt.release();
+    if (segs.empty() || !have_device()) return;
+    const size_t sb = segs.size() * sizeof(Seg), tb = tiles.size() * sizeof(uint32_t);
+    if (hipMalloc(&dt.segs, sb) != hipSuccess) throw hip_error("hipMalloc(segments)");
+    if (hipMalloc(reinterpret_cast<void**>(&dt.tiles), tb) != hipSuccess)
+        throw hip_error("hipMalloc(tiles)");
+    if (hipMemcpy(dt.segs, segs.data(), sb, hipMemcpyHostToDevice) != hipSuccess)
+        throw hip_error("hipMemcpy(segments)");
+    if (hipMemcpy(dt.tiles, tiles.data(), tb, hipMemcpyHostToDevice) != hipSuccess)
+        throw hip_error("hipMemcpy(tiles)");
+}
+}  // namespace
+
+void device_tables::release()
+{
+    if (segs) (void)hipFree(segs);
+    if (tiles) (void)hipFree(tiles);
+    if (lids) (void)hipFree(lids);
+    segs = nullptr;
+    tiles = nullptr;
+    lids = nullptr;
+}
+
+// ---------------------------------------------------------------------------------------------
+// structured
+// ---------------------------------------------------------------------------------------------
+void validate_field(const ghx_field_desc& f)
+{
+    if (f.dim < 1 || f.dim > GHX_MAX_DIM) throw invalid("field dim must be in [1, 4]");
+    if (f.elem_size < 1) throw invalid("elem_size must be >= 1");
+    if (f.num_components < 1) throw invalid("number of components must be greater than 0");
+    if (!f.has_components && f.num_components > 1)
+        throw invalid("this field cannot have more than 1 components");
+    if (f.has_components && f.dim < 2) throw invalid("component axis needs dim >= 2");
+    bool seen[GHX_MAX_DIM] = {false, false, false, false};
+    for (int d = 0; d < f.dim; ++d)
+    {
+        if (f.layout[d] < 0 || f.layout[d] >= f.dim || seen[f.layout[d]])
+            throw invalid("layout must be a permutation of 0..dim-1");
+        seen[f.layout[d]] = true;
+    }
+}
+
+// Append the segments of one iteration space (`box`, spatial dims only).
+// Mirrors make_pack_is / make_buffer_desc / make_is (regular/field_descriptor.hpp:114-150):
+// the buffer box is dense in the field's layout order; row = run along the layout's stride-1
+// dim. Returns the buffer bytes of the space (is.size() * num_components * sizeof(T)).
+uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, const ghx_box& box,
+                          uint16_t field_slot, uint16_t buf_slot, uint64_t buf_off)
+{
+    const int D = f.dim;
+    const int spatial = D - (f.has_components ? 1 : 0);
+    int64_t first[GHX_MAX_DIM], ext[GHX_MAX_DIM];
+    for (int d = 0; d < D; ++d)
+    {
+        if (d < spatial)
+        {
+            first[d] = box.first[d];
+            ext[d] = int64_t(box.last[d]) - box.first[d] + 1;
+        }
+        else
+        {
+            first[d] = 0;
+            ext[d] = f.num_components;
+        }
+        if (ext[d] <= 0) throw invalid("iteration space: first must be <= last");
+        // bounds against the declared extents (the reference does not check; a GPU fault here
+        // would take the whole node down, so the planner refuses instead)
+        const int64_t off = d < spatial ? f.offsets[d] : 0;
+        if (f.extents[d] > 0 && (first[d] + off < 0 || first[d] + ext[d] - 1 + off >= f.extents[d]))
+            throw invalid("iteration space outside the field extents");
+    }
+    int64_t n = 1;
+    for (int d = 0; d < D; ++d) n *= ext[d];
+    const int64_t elem = f.elem_size;
+    // dims sorted by layout value, fastest (value D-1) first
+    int by_speed[GHX_MAX_DIM];
+    for (int d = 0; d < D; ++d) by_speed[D - 1 - f.layout[d]] = d;
+    const int cont = by_speed[0];
+    int64_t L;
+    int outer[GHX_MAX_DIM + 1];
+    int n_outer = 0;
+    if (f.byte_strides[cont] == elem)
+    {
+        L = ext[cont] * elem;
+        for (int k = 1; k < D; ++k) outer[n_outer++] = by_speed[k];
+    }
+    else
+    {
+        // strided fastest dim: every element is its own row (element-wise semantics of the GPU
+        // reference, pack_kernels.hpp:161-183)
+        L = elem;
+        for (int k = 0; k < D; ++k) outer[n_outer++] = by_speed[k];
+    }
+    int64_t ostride[GHX_MAX_DIM], oext[GHX_MAX_DIM];
+    for (int k = 0; k < n_outer; ++k)
+    {
+        ostride[k] = f.byte_strides[outer[k]];
+        oext[k] = ext[outer[k]];
+    }
+    // merge rows that are contiguous in the field too (box spans the full padded run)
+    while (n_outer > 0 && ostride[0] == L && oext[0] * L < (int64_t(1) << 30))
+    {
+        L *= oext[0];
+        for (int k = 1; k < n_outer; ++k)
+        {
+            ostride[k - 1] = ostride[k];
+            oext[k - 1] = oext[k];
+        }
+        --n_outer;
+    }
+    if (n_outer > 4) throw invalid("too many outer dims");
+    if (L >= (int64_t(1) << 31)) throw invalid("row too long");
+    int64_t field_off = 0;
+    for (int d = 0; d < D; ++d)
+    {
+        const int64_t off = d < spatial ? f.offsets[d] : 0;
+        field_off += (first[d] + off) * f.byte_strides[d];
+    }
+    // split along the slowest outer dim so that one segment stays below 2^31 bytes
+    int64_t rows_per_slowest = 1;
+    for (int k = 0; k + 1 < n_outer; ++k) rows_per_slowest *= oext[k];
+    const int64_t slab = rows_per_slowest * L;  // bytes per unit of the slowest outer dim
+    const int64_t nslow = n_outer > 0 ? oext[n_outer - 1] : 1;
+    const int64_t max_bytes = (int64_t(1) << 31) - kTileBytes;
+    int64_t chunk = n_outer > 0 ? std::max<int64_t>(1, max_bytes / slab) : 1;
+    if (n_outer == 0 && L > max_bytes) throw invalid("segment too large");
+    if (n_outer > 0 && slab > max_bytes) throw invalid("segment row block too large");
+    for (int64_t s0 = 0; s0 < nslow; s0 += chunk)
+    {
+        const int64_t cnt = std::min(chunk, nslow - s0);
+        seg_s s{};
+        s.field_slot = field_slot;
+        s.buf_slot = buf_slot;
+        s.row_bytes = uint32_t(L);
+        s.n_outer = uint8_t(n_outer);
+        int64_t rows = 1;
+        for (int k = 0; k < 4; ++k)
+        {
+            if (k < n_outer)
+            {
+                s.stride[k] = ostride[k];
+                s.ext[k] = uint32_t(k == n_outer - 1 ? cnt : oext[k]);
+            }
+            else
+            {
+                s.stride[k] = 0;
+                s.ext[k] = 1;
+            }
+            rows *= s.ext[k];
+        }
+        s.field_off = field_off + (n_outer > 0 ? s0 * ostride[n_outer - 1] : 0);
+        s.buf_off = buf_off + uint64_t(s0 * slab);
+        s.bytes = uint32_t(rows * L);
+        s.mag_row = make_magic(uint32_t(L));
+        for (int k = 0; k < 3; ++k) s.mag_ext[k] = make_magic(s.ext[k]);
+        int w = wlog2_of(uint64_t(L));
+        w = std::min(w, wlog2_of(uint64_t(s.field_off)));
+        w = std::min(w, wlog2_of(s.buf_off));
+        for (int k = 0; k < n_outer; ++k)
+            if (s.ext[k] > 1) w = std::min(w, wlog2_of(uint64_t(s.stride[k] < 0 ? -s.stride[k] : s.stride[k])));
+        s.wlog2 = uint8_t(w);
+        out.push_back(s);
+    }
+    return uint64_t(n * elem);
+}
+
+splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(dir)
+{
+    if (dir != 0 && dir != 1) throw invalid("direction must be 0 (pack) or 1 (unpack)");
+    std::vector<seg_s> segs;
+    for (int e = 0; e < n_entries; ++e)
+    {
+        const auto& en = entries[e];
+        validate_field(en.field);
+        if (en.field_slot < 0 || en.field_slot >= GHX_MAX_SLOTS || en.buffer_slot < 0 ||
+            en.buffer_slot >= GHX_MAX_SLOTS)
+            throw invalid("slot out of range [0, 64)");
+        if (en.n_boxes < 0 || (en.n_boxes > 0 && !en.boxes)) throw invalid("bad boxes");
+        max_field_slot = std::max(max_field_slot, en.field_slot);
+        max_buf_slot = std::max(max_buf_slot, en.buffer_slot);
+        uint64_t off = en.buffer_offset;
+        for (int b = 0; b < en.n_boxes; ++b)
+            off += add_box_segments(segs, en.field, en.boxes[b], uint16_t(en.field_slot),
+                                    uint16_t(en.buffer_slot), off);
+        bytes += off - en.buffer_offset;
+    }
+    std::vector<uint32_t> tiles;
+    for (uint32_t i = 0; i < segs.size(); ++i)
+    {
+        segs[i].first_tile = uint32_t(tiles.size());
+        const uint32_t nt = tiles_of(segs[i].bytes);
+        for (uint32_t t = 0; t < nt; ++t) tiles.push_back(i);
+    }
+    n_segments = int32_t(segs.size());
+    n_tiles = uint32_t(tiles.size());
+    host_segs = segs;
+    upload(dev, segs, tiles);
+}
+
+int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* stream) const
+{
+    if (n_tiles == 0) return GHX_OK;
+    if (nf <= max_field_slot || nb <= max_buf_slot) throw invalid("pointer arrays do not cover the plan's slots");
+    if (!dev.segs) throw hip_error("plan has no device tables (no HIP device at creation)");
+    kargs a{};
+    a.segs = dev.segs;
+    a.tile_seg = dev.tiles;
+    a.n_tiles = n_tiles;
+    for (int i = 0; i <= max_field_slot; ++i)
+    {
+        if (!fptr[i]) throw invalid("null field pointer");
+        a.field_ptr[i] = reinterpret_cast<uint64_t>(fptr[i]);
+    }
+    for (int i = 0; i <= max_buf_slot; ++i)
+    {
+        if (!bptr[i]) throw invalid("null buffer pointer");
+        a.buf_ptr[i] = reinterpret_cast<uint64_t>(bptr[i]);
+    }
+    return launch_structured(a, direction, stream, grid_for_tiles(n_tiles));
+}
+
+// ---------------------------------------------------------------------------------------------
+// unstructured
+// ---------------------------------------------------------------------------------------------
+uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction(dir)
+{
+    if (dir != 0 && dir != 1) throw invalid("direction must be 0 (pack) or 1 (unpack)");
+    std::vector<seg_u> segs;
+    // all index lists in one device allocation: int32 where they fit
+    struct pending
+    {
+        size_t seg;
+        const int64_t* lids;
+        int64_t n;
+        bool wide;
+        size_t off;
+    };
+    std::vector<pending> pend;
+    size_t lid_bytes = 0;
+    for (int e = 0; e < n_entries; ++e)
+    {
+        const auto& en = entries[e];
+        const auto& d = en.data;
+        if (d.elem_size < 1 || d.levels < 1) throw invalid("bad unstructured data descriptor");
+        if (en.field_slot < 0 || en.field_slot >= GHX_MAX_SLOTS || en.buffer_slot < 0 ||
+            en.buffer_slot >= GHX_MAX_SLOTS)
+            throw invalid("slot out of range [0, 64)");
+        if (en.n_lids < 0 || (en.n_lids > 0 && !en.lids)) throw invalid("bad index list");
+        max_field_slot = std::max(max_field_slot, en.field_slot);
+        max_buf_slot = std::max(max_buf_slot, en.buffer_slot);
+        if (en.n_lids == 0) continue;
+        const int64_t elem = d.elem_size;
+        const int64_t total = en.n_lids * d.levels * elem;
+        if (total >= (int64_t(1) << 31) - kTileBytes || en.n_lids >= (int64_t(1) << 32))
+            throw invalid("unstructured segment too large");
+        bool wide = false;
+        for (int64_t i = 0; i < en.n_lids; ++i)
+        {
+            if (en.lids[i] < 0) throw invalid("negative local index");
+            if (en.lids[i] >= (int64_t(1) << 31)) wide = true;
+        }
+        seg_u s{};
+        s.field_slot = uint16_t(en.field_slot);
+        s.buf_slot = uint16_t(en.buffer_slot);
+        s.buf_off = en.buffer_offset;
+        s.n = uint32_t(en.n_lids);
+        s.index_stride_b = d.index_stride * elem;
+        s.level_stride_b = d.level_stride * elem;
+        s.lid64 = wide ? 1 : 0;
+        int64_t L;
+        if (d.levels == 1 || (d.levels_first && d.level_stride == 1))
+        {
+            s.mode = 0;  // one row per index: all levels contiguous on both sides
+            L = d.levels * elem;
+        }
+        else if (d.levels_first)
+        {
+            s.mode = 1;  // buf[(i*levels + l)]: rows (i, l), i-major
+            L = elem;
+            s.row_levels = uint32_t(d.levels);
+            s.mag_inner = make_magic(uint32_t(d.levels));
+        }
+        else
+        {
+            s.mode = 2;  // buf[(l*n + i)]: rows (l, i), l-major
+            L = elem;
+            s.mag_inner = make_magic(uint32_t(en.n_lids));
+        }
+        s.row_bytes = uint32_t(L);
+        s.bytes = uint32_t(total);
+        s.mag_row = make_magic(uint32_t(L));
+        int w = wlog2_of(uint64_t(L));
+        w = std::min(w, wlog2_of(s.buf_off));
+        if (en.n_lids > 1) w = std::min(w, wlog2_of(uint64_t(s.index_stride_b < 0 ? -s.index_stride_b : s.index_stride_b)));
+        if (s.mode != 0) w = std::min(w, wlog2_of(uint64_t(s.level_stride_b < 0 ? -s.level_stride_b : s.level_stride_b)));
+        s.wlog2 = uint8_t(w);
+        lid_bytes = (lid_bytes + 15) & ~size_t(15);
+        pend.push_back({segs.size(), en.lids, en.n_lids, wide, lid_bytes});
+        lid_bytes += size_t(en.n_lids) * (wide ? 8 : 4);
+        segs.push_back(s);
+        bytes += uint64_t(total);
+    }
+    std::vector<uint32_t> tiles;
+    for (uint32_t i = 0; i < segs.size(); ++i)
+    {
+        segs[i].first_tile = uint32_t(tiles.size());
+        const uint32_t nt = tiles_of(segs[i].bytes);
+        for (uint32_t t = 0; t < nt; ++t) tiles.push_back(i);
+    }
+    n_segments = int32_t(segs.size());
+    n_tiles = uint32_t(tiles.size());
+    if (!segs.empty() && have_device())
+    {
+        std::vector<unsigned char> host(lid_bytes);
+        for (auto& p : pend)
+        {
+            if (p.wide) std::memcpy(host.data() + p.off, p.lids, size_t(p.n) * 8);
+            else
+            {
+                int32_t* dst = reinterpret_cast<int32_t*>(host.data() + p.off);
+                for (int64_t i = 0; i < p.n; ++i) dst[i] = int32_t(p.lids[i]);
+            }
+        }
+        if (hipMalloc(&dev.lids, lid_bytes) != hipSuccess) throw hip_error("hipMalloc(lids)");
+        if (hipMemcpy(dev.lids, host.data(), lid_bytes, hipMemcpyHostToDevice) != hipSuccess)
+            throw hip_error("hipMemcpy(lids)");
+        for (auto& p : pend) segs[p.seg].lids = static_cast<char*>(dev.lids) + p.off;
+        void* keep = dev.lids;
+        dev.lids = nullptr;  // upload() releases; re-attach after
+        upload(dev, segs, tiles);
+        dev.lids = keep;
+    }
+}
+
+int uplan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* stream) const
+{
+    if (n_tiles == 0) return GHX_OK;
+    if (nf <= max_field_slot || nb <= max_buf_slot) throw invalid("pointer arrays do not cover the plan's slots");
+    if (!dev.segs) throw hip_error("plan has no device tables (no HIP device at creation)");
+    kargs a{};
+    a.segs = dev.segs;
+    a.tile_seg = dev.tiles;
+    a.n_tiles = n_tiles;
+    for (int i = 0; i <= max_field_slot; ++i)
+    {
+        if (!fptr[i]) throw invalid("null field pointer");
+        a.field_ptr[i] = reinterpret_cast<uint64_t>(fptr[i]);
+    }
+    for (int i = 0; i <= max_buf_slot; ++i)
+    {
+        if (!bptr[i]) throw invalid("null buffer pointer");
+        a.buf_ptr[i] = reinterpret_cast<uint64_t>(bptr[i]);
+    }
+    return launch_unstructured(a, direction, stream, grid_for_tiles(n_tiles));
+}
+
+}  // namespace ghx

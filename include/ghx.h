@@ -1,0 +1,269 @@
+/*
+ * ghx.h — C ABI of ghex_amd, the MI355X-native halo pack/unpack path for GHEX.
+ *
+ * Plain C: pointers, sizes and status codes only (no C++ or torch types cross this line).
+ * The library is libghx.so (ghex_amd/lib/). Every entry point below names the reference
+ * interface it replaces (paths relative to the GHEX v0.8.0 tree). INTEGRATION.md shows the
+ * binding a GHEX maintainer would add on the reference side.
+ *
+ * Status: every function returns GHX_OK (0) or a negative ghx_status; ghx_last_error() then
+ * returns a thread-local message. No exception crosses the ABI (the reference throws
+ * std::runtime_error, include/ghex/device/cuda/error.hpp:21-25; the C++ adaptor in
+ * include/ghex_amd/field_descriptor.hpp converts back to that convention).
+ *
+ * Threading: plans and patterns are immutable after creation; executing one plan from several
+ * threads on distinct streams is safe. Executions are stream-ordered and asynchronous (no host
+ * synchronisation inside ghx_*_execute / ghx_*_pack / ghx_*_unpack), so they can be captured
+ * into a hipGraph.
+ */
+#ifndef GHX_H
+#define GHX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum ghx_status
+{
+    GHX_OK = 0,
+    GHX_ERR_INVALID = -1,    /* bad argument (shape, layout, slot, alignment ...) */
+    GHX_ERR_HIP = -2,        /* a HIP runtime call failed */
+    GHX_ERR_NOMEM = -3,      /* host or device allocation failed */
+    GHX_ERR_PATTERN = -4,    /* pattern construction failed (e.g. inconsistent halo gids) */
+} ghx_status;
+
+/* Opaque stream handle: a hipStream_t (NULL = the default stream). Kept as void* so that this
+ * header needs no HIP include. Replaces the `void* arg` = cudaStream_t* of the reference's
+ * field-descriptor concept (include/ghex/structured/pack_kernels.hpp:216-234). */
+typedef void* ghx_stream;
+
+#define GHX_MAX_DIM 4     /* 3 spatial dims + 1 component axis (bindings/python/src/_pyghex/structured/types.hpp:31-63) */
+#define GHX_MAX_SLOTS 64  /* field / buffer pointer slots per plan execution */
+
+/* Last error message of the calling thread ("" if none). */
+const char* ghx_last_error(void);
+/* Library version string and the offload target it was compiled for ("gfx950"). */
+const char* ghx_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Structured fields
+ * ------------------------------------------------------------------------------------------ */
+
+/* A wrapped structured field: the queries of the reference's field-descriptor concept
+ * (doc_src/scope/scope.rst:331-359; include/ghex/structured/field_descriptor.hpp:27-41,
+ * 152-226): dimension (incl. component axis), value size, layout_map, byte strides, offsets.
+ * layout[d] = gridtools::layout_map<...>::at(d); the dim whose value is dim-1 is stride-1.
+ * has_components: the last dim is the component axis of extent num_components (offset 0). */
+typedef struct ghx_field_desc
+{
+    int32_t dim;
+    int32_t elem_size;                 /* sizeof(value_type), any size >= 1 */
+    int32_t layout[GHX_MAX_DIM];
+    int64_t byte_strides[GHX_MAX_DIM];
+    int32_t offsets[GHX_MAX_DIM];
+    int32_t extents[GHX_MAX_DIM];      /* informational (bounds checks), incl. halos */
+    int32_t num_components;            /* >= 1 */
+    int32_t has_components;            /* 0/1 */
+} ghx_field_desc;
+
+/* One iteration space in the field's local coordinates: pattern::iteration_space_pair::local()
+ * (include/ghex/structured/pattern.hpp:44-120). Only the spatial dims are given; the component
+ * axis is added as [0, num_components-1] (regular/field_descriptor.hpp:131-150). */
+typedef struct ghx_box
+{
+    int32_t first[GHX_MAX_DIM];
+    int32_t last[GHX_MAX_DIM];
+} ghx_box;
+
+/* One (field, list of iteration spaces) placed into one buffer at a byte offset: the
+ * communication object's field_info (include/ghex/communication_object.hpp:176-188, 1059-1065). */
+typedef struct ghx_pack_entry
+{
+    ghx_field_desc field;
+    int32_t field_slot;                /* index into field_ptrs[] at execution */
+    int32_t buffer_slot;               /* index into buffer_ptrs[] at execution */
+    uint64_t buffer_offset;            /* byte offset of this field's data in that buffer */
+    const ghx_box* boxes;              /* iteration spaces, in pattern order */
+    int32_t n_boxes;
+} ghx_pack_entry;
+
+typedef struct ghx_plan ghx_plan;
+
+/* Build a fused pack (direction 0) or unpack (direction 1) plan over many fields, iteration
+ * spaces and buffers: ONE kernel launch per execution. Replaces the per-iteration-space launch
+ * loop of regular::field_descriptor::pack/unpack (include/ghex/structured/regular/field_descriptor.hpp:72-96)
+ * -> serialization<gpu,L>::pack/unpack (include/ghex/structured/pack_kernels.hpp:161-248), the
+ * batched pack_kernel_u of packer<gpu>::pack_u (include/ghex/packer.hpp:98-121, 192-297), and
+ * packer<gpu>::pack/unpack over all buffers of communication_object::pack
+ * (include/ghex/communication_object.hpp:568-597; packer.hpp:124-190).
+ * The packed byte layout is bit-identical to serialization<cpu>::pack_batch. Descriptor tables
+ * are uploaded to device memory here (synchronously); execution never allocates. */
+int ghx_plan_create(const ghx_pack_entry* entries, int32_t n_entries, int32_t direction,
+                    ghx_plan** out);
+/* Enqueue the plan on `stream`: pack = buffers <- fields, unpack = fields <- buffers.
+ * field_ptrs/buffer_ptrs are device pointers indexed by slot (n_field_ptrs/n_buffer_ptrs must
+ * cover every slot the plan uses). */
+int ghx_plan_execute(const ghx_plan* plan, void* const* field_ptrs, int32_t n_field_ptrs,
+                     void* const* buffer_ptrs, int32_t n_buffer_ptrs, ghx_stream stream);
+int ghx_plan_destroy(ghx_plan* plan);
+/* Plan facts: total buffer bytes moved per execution, number of segments (field x iteration
+ * space), number of workgroup tiles, and the largest byte offset+size touched per buffer slot. */
+int ghx_plan_info(const ghx_plan* plan, uint64_t* bytes, int32_t* n_segments, int32_t* n_tiles);
+
+/* The reference's field.pack(T* buffer, const IndexContainer& c, void* arg)
+ * (include/ghex/structured/regular/field_descriptor.hpp:72-83) for ONE field: iteration spaces
+ * back to back from `buffer`. Convenience form of plan_create+execute (the descriptor upload is
+ * stream-ordered from a pinned staging copy; prefer a cached plan in a loop). */
+int ghx_structured_pack(const ghx_field_desc* field, const void* field_data, void* buffer,
+                        const ghx_box* boxes, int32_t n_boxes, ghx_stream stream);
+/* field.unpack(const T* buffer, const IndexContainer& c, void* arg)
+ * (include/ghex/structured/regular/field_descriptor.hpp:85-96). */
+int ghx_structured_unpack(const ghx_field_desc* field, void* field_data, const void* buffer,
+                          const ghx_box* boxes, int32_t n_boxes, ghx_stream stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Unstructured fields (index-list gather / scatter)
+ * ------------------------------------------------------------------------------------------ */
+
+/* unstructured::data_descriptor<gpu> (include/ghex/unstructured/user_concepts.hpp:526-577):
+ * value(lid, level) at values + (lid*index_stride + level*level_stride)*elem_size. */
+typedef struct ghx_udata_desc
+{
+    int32_t elem_size;
+    int32_t levels;
+    int32_t levels_first;              /* buffer order: levels_first ? [i][level] : [level][i] */
+    int64_t index_stride;              /* in elements */
+    int64_t level_stride;              /* in elements */
+} ghx_udata_desc;
+
+typedef struct ghx_upack_entry
+{
+    ghx_udata_desc data;
+    int32_t field_slot;
+    int32_t buffer_slot;
+    uint64_t buffer_offset;
+    const int64_t* lids;               /* HOST array of local indices (pattern order); copied to
+                                          device memory as int32 (int64 if any lid >= 2^31) */
+    int64_t n_lids;
+} ghx_upack_entry;
+
+typedef struct ghx_uplan ghx_uplan;
+
+/* Fused unstructured pack (0) / unpack (1) plan: replaces data_descriptor<gpu>::pack/unpack
+ * and the four pack/unpack_kernel_levels_{first,last} launches per neighbour
+ * (include/ghex/unstructured/user_concepts.hpp:455-523, 583-666). Index lists live in
+ * device memory (not managed memory as in unstructured/pattern.hpp:53-57). */
+int ghx_uplan_create(const ghx_upack_entry* entries, int32_t n_entries, int32_t direction,
+                     ghx_uplan** out);
+int ghx_uplan_execute(const ghx_uplan* plan, void* const* field_ptrs, int32_t n_field_ptrs,
+                      void* const* buffer_ptrs, int32_t n_buffer_ptrs, ghx_stream stream);
+int ghx_uplan_destroy(ghx_uplan* plan);
+int ghx_uplan_info(const ghx_uplan* plan, uint64_t* bytes, int32_t* n_segments, int32_t* n_tiles);
+
+/* ------------------------------------------------------------------------------------------
+ * Patterns (setup time, host only): the producers of the pack inputs.
+ * ------------------------------------------------------------------------------------------ */
+
+/* One rank's domains for pattern construction, given for ALL ranks (the reference obtains them
+ * with MPI all_gather, include/ghex/structured/pattern.hpp:268-273). */
+typedef struct ghx_regular_domain
+{
+    int32_t id;
+    int32_t rank;
+    int32_t first[3];
+    int32_t last[3];
+} ghx_regular_domain;
+
+typedef struct ghx_pattern ghx_pattern;
+
+/* halo_generator::operator() (include/ghex/structured/regular/halo_generator.hpp:93-148):
+ * receive boxes of one domain, in the reference's order. Writes up to max_boxes boxes
+ * (local first/last into `local`, global first/last into `global`), returns the count in
+ * *n_boxes (call with max_boxes = 0 to query). halos = (dim0-, dim0+, dim1-, dim1+, ...). */
+int ghx_regular_halo_boxes(int32_t dim, const int32_t* global_first, const int32_t* global_last,
+                           const int32_t* halos, const int32_t* periodic,
+                           const int32_t* domain_first, const int32_t* domain_last,
+                           ghx_box* local, ghx_box* global, int32_t max_boxes, int32_t* n_boxes);
+
+/* make_pattern<structured::grid> (include/ghex/structured/pattern.hpp:214-571), computed for
+ * rank `my_rank` from all ranks' domains (ordered by rank, then each rank's d_range order). */
+int ghx_regular_pattern_create(int32_t dim, const ghx_regular_domain* domains,
+                               int32_t n_domains, const int32_t* global_first,
+                               const int32_t* global_last, const int32_t* halos,
+                               const int32_t* periodic, int32_t my_rank, ghx_pattern** out);
+
+/* make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370) for rank
+ * `my_rank`. For every domain d of every rank: gids[d] (storage order), the outer (halo) local
+ * ids, and optionally the halo generator's gid list (NULL/-1 = all outer gids,
+ * user_concepts.hpp:244-252). Arrays are concatenated; *_count give per-domain lengths. */
+int ghx_unstructured_pattern_create(int32_t n_domains, const int32_t* domain_ids,
+                                    const int32_t* domain_ranks, const int64_t* gids,
+                                    const int64_t* gid_counts, const int64_t* outer_lids,
+                                    const int64_t* outer_counts, const int64_t* halo_gids,
+                                    const int64_t* halo_counts, int32_t my_rank,
+                                    ghx_pattern** out);
+
+int ghx_pattern_destroy(ghx_pattern* p);
+/* Number of local domains (patterns) of this rank, and the global max tag
+ * (pattern_container::max_tag, include/ghex/pattern_container.hpp:78-83). */
+int ghx_pattern_num_domains(const ghx_pattern* p, int32_t* n);
+int ghx_pattern_max_tag(const ghx_pattern* p, int32_t* max_tag);
+int ghx_pattern_domain_id(const ghx_pattern* p, int32_t local_index, int32_t* id);
+/* Halo maps of local domain `local_index`: direction 0 = send_halos(), 1 = recv_halos(),
+ * in std::map key order. Key k: remote domain id, remote rank, tag, #iteration spaces and
+ * #elements (spatial). */
+int ghx_pattern_num_keys(const ghx_pattern* p, int32_t local_index, int32_t direction,
+                         int32_t* n_keys);
+int ghx_pattern_key(const ghx_pattern* p, int32_t local_index, int32_t direction, int32_t key,
+                    int32_t* remote_id, int32_t* remote_rank, int32_t* tag, int32_t* n_spaces,
+                    int64_t* n_elements);
+/* Structured: the iteration spaces of a key (local and global boxes). */
+int ghx_pattern_key_boxes(const ghx_pattern* p, int32_t local_index, int32_t direction,
+                          int32_t key, ghx_box* local, ghx_box* global, int32_t max_boxes);
+/* Unstructured: the local index list of a key (its single iteration space). */
+int ghx_pattern_key_lids(const ghx_pattern* p, int32_t local_index, int32_t direction,
+                         int32_t key, int64_t* lids, int64_t max_lids);
+
+/* ------------------------------------------------------------------------------------------
+ * Exchange planning: communication_object::allocate semantics (buffer per domain pair, fields
+ * in exchange() order, alignof padding, tag = pattern tag + container tag offset)
+ * (include/ghex/communication_object.hpp:483-566, 1003-1067).
+ * ------------------------------------------------------------------------------------------ */
+
+typedef struct ghx_exchange_item
+{
+    const ghx_pattern* pattern;        /* the field's pattern container (this rank) */
+    int32_t local_index;               /* which local domain of that pattern */
+    int32_t kind;                      /* 0 = structured (field), 1 = unstructured (udata) */
+    ghx_field_desc field;              /* kind 0 */
+    ghx_udata_desc udata;              /* kind 1 */
+    int32_t align;                     /* alignof(value_type) */
+    int32_t tag_offset;                /* prepare_exchange_buffers tag map (:540-549) */
+} ghx_exchange_item;
+
+typedef struct ghx_exchange ghx_exchange;
+
+/* Plans one exchange() of n_items fields (field_slot = item index). Produces the send and recv
+ * buffer lists (std::map order of domain_id_pair) and fused pack / unpack plans over them
+ * (buffer_slot = buffer index). */
+int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exchange** out);
+int ghx_exchange_destroy(ghx_exchange* ex);
+/* direction 0 = send buffers, 1 = recv buffers. */
+int ghx_exchange_num_buffers(const ghx_exchange* ex, int32_t direction, int32_t* n);
+int ghx_exchange_buffer(const ghx_exchange* ex, int32_t direction, int32_t index,
+                        int32_t* first_id, int32_t* second_id, int32_t* rank, int32_t* tag,
+                        uint64_t* size);
+/* Enqueue the fused pack of all send buffers / fused unpack of all recv buffers. */
+int ghx_exchange_pack(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                      void* const* send_buffers, int32_t n_send, ghx_stream stream);
+int ghx_exchange_unpack(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                        void* const* recv_buffers, int32_t n_recv, ghx_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GHX_H */

@@ -1,0 +1,206 @@
+"""CPU tests of the product's host side (no GPU): the C-ABI library loads and exports every
+declared symbol; patterns and exchange buffer plans computed by libghx equal the oracle's
+(which is pinned to the reference, tests/test_oracle.py)."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests import helpers as H
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ghx():
+    from ghex_amd import _ghx
+    return _ghx
+
+
+def test_library_exports_every_declared_symbol(ghx):
+    L = ghx.lib()
+    with open(os.path.join(ROOT, "include", "ghx.h")) as fh:
+        decl = set(re.findall(r"^(?:int|const char\*)\s+(ghx_\w+)\s*\(", fh.read(), re.M))
+    assert len(decl) >= 25
+    missing = [n for n in decl if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(ghx.EXPORTED) == decl, set(ghx.EXPORTED) ^ decl
+    assert b"gfx950" in L.ghx_version()
+
+
+def test_library_is_built_for_gfx950():
+    so = os.path.join(ROOT, "ghex_amd", "lib", "libghx.so")
+    data = open(so, "rb").read()
+    assert b"gfx950" in data
+    assert b"oracle" not in data.lower().replace(b"ghex_amd", b"")  # product never links the oracle
+
+
+def test_errors_are_reported_not_thrown(ghx):
+    h = ctypes.c_void_p()
+    rc = ghx.lib().ghx_regular_pattern_create(7, None, 0, None, None, None, None, 0,
+                                              ctypes.byref(h))
+    assert rc == -1
+    assert b"null" in ghx.lib().ghx_last_error() or b"dim" in ghx.lib().ghx_last_error()
+
+
+def test_halo_boxes_via_abi_match_reference(golden_dir):
+    from ghex_amd.structured.regular import DomainDescriptor, HaloGenerator
+    with open(os.path.join(golden_dir, "ref_halo_boxes.json")) as fh:
+        cfgs = json.load(fh)["configs"]
+    for c in cfgs:
+        hg = HaloGenerator(c["gfirst"], c["glast"], c["halos"], c["periodic"])
+        got = hg(DomainDescriptor(0, c["dom"][0], c["dom"][1]))
+        exp = c["boxes"]
+        assert [list(a) + list(b) + list(g) + list(h) for a, b, g, h in got] == exp
+
+
+def _regular_pattern_abi(ranks, gf, gl, halos, periodic, my_rank):
+    from ghex_amd.structured.regular import DomainDescriptor, HaloGenerator, make_pattern
+
+    class FakeCtx:
+        def __init__(self, r, n):
+            self.r, self.n = r, n
+
+        def rank(self):
+            return self.r
+
+        def size(self):
+            return self.n
+
+        def all_gather_object(self, obj):
+            return [[(d.id, d.first, d.last) for d in doms] for doms in ranks]
+
+    hg = HaloGenerator(gf, gl, halos, periodic)
+    mine = [DomainDescriptor(d.id, d.first, d.last) for d in ranks[my_rank]]
+    return make_pattern(FakeCtx(my_rank, len(ranks)), hg, mine)
+
+
+def _cmp_regular(pc, opats, D):
+    assert len(pc) == len(opats)
+    for li, op in enumerate(opats):
+        for direction, omap in ((0, op.send_items()), (1, op.recv_items())):
+            got = pc.halos(li, direction)
+            assert len(got) == len(omap)
+            for (rid, rr, tag, spaces), ((oid, otag), (orank, lst)) in zip(got, omap):
+                assert (rid, tag, rr) == (oid, otag, orank)
+                assert [(a, b, c, d) for a, b, c, d in spaces] == \
+                    [(isp.lf, isp.ll, isp.gf, isp.gl) for isp in lst]
+        assert pc.max_tag() == op.max_tag
+
+
+@pytest.mark.parametrize("halos", [H.HALOS_1, H.HALOS_2])
+def test_regular_pattern_reference_geometry(halos):
+    ranks, gf, gl = H.regular_test_domains(4)
+    opat = orc.regular_make_pattern(ranks, gf, gl, halos, (1, 1, 1))
+    for r in range(4):
+        pc = _regular_pattern_abi(ranks, gf, gl, halos, (1, 1, 1), r)
+        _cmp_regular(pc, opat[r], 3)
+
+
+@pytest.mark.parametrize("parts", [(1, 1, 1), (2, 1, 1), (2, 2, 1), (2, 2, 2), (3, 2, 1)])
+@pytest.mark.parametrize("halos,periodic", [((1,) * 6, (1, 1, 1)), ((2, 1, 1, 2, 0, 3), (1, 1, 1)),
+                                            ((2,) * 6, (0, 1, 0))])
+def test_regular_pattern_cubes(parts, halos, periodic):
+    ranks, gf, gl = H.cube_domains(6, parts)
+    opat = orc.regular_make_pattern(ranks, gf, gl, halos, periodic)
+    for r in range(len(ranks)):
+        pc = _regular_pattern_abi(ranks, gf, gl, halos, periodic, r)
+        _cmp_regular(pc, opat[r], 3)
+
+
+def _unstructured_abi(doms_ranks, halo_gids, my_rank):
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
+
+    class FakeCtx:
+        def rank(self):
+            return my_rank
+
+        def size(self):
+            return len(doms_ranks)
+
+        def all_gather_object(self, obj):
+            out = []
+            for r, doms in enumerate(doms_ranks):
+                out.append([(d.id, d.gids, d.outer_lids,
+                             None if halo_gids is None else halo_gids[r][i])
+                            for i, d in enumerate(doms)])
+            return out
+
+    mine = [DomainDescriptor(d.id, d.gids, d.outer_lids) for d in doms_ranks[my_rank]]
+    hg = HaloGenerator(None if halo_gids is None else halo_gids[my_rank][0])
+    return make_pattern(FakeCtx(), hg, mine)
+
+
+class _UD:
+    def __init__(self, id_, gids, outer_lids):
+        self.id, self.gids, self.outer_lids = id_, gids, outer_lids
+
+
+def test_unstructured_pattern_known_answer(golden_dir):
+    with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
+        case = json.load(fh)
+    doms = [[_UD(int(k), v["gids"], v["halo_lids"])] for k, v in sorted(case["domains"].items())]
+    for r in range(4):
+        pc = _unstructured_abi(doms, None, r)
+        sends = {str(rid): lids for rid, rr, tag, lids in pc.send_halos(0)}
+        recvs = {str(rid): lids for rid, rr, tag, lids in pc.recv_halos(0)}
+        assert sends == case["send_maps"][str(r)]
+        assert recvs == case["recv_maps"][str(r)]
+
+
+def test_unstructured_pattern_matches_oracle_with_repeats(golden_dir):
+    with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
+        fx = json.load(fh)["python_fixture"]
+    items = sorted(fx["domains"].items())
+    doms = [[_UD(int(k), v["all"], v["outer_lids"])] for k, v in items]
+    hg = [[v["outer"]] for k, v in items]
+    odoms = [[orc.UnstructuredDomain(int(k), v["all"], v["outer_lids"])] for k, v in items]
+    opats = orc.unstructured_make_pattern(odoms, hg)
+    for r in range(4):
+        pc = _unstructured_abi(doms, hg, r)
+        for direction, key in ((0, "send"), (1, "recv")):
+            got = [(rr, tag, rid, lids) for rid, rr, tag, lids in pc.halos(0, direction)]
+            exp = [(rr, tag, rid, lids) for (rr, tag), (rid, lids) in opats[r][0][key].items()]
+            assert got == exp
+        assert pc.max_tag() == 0 or pc.max_tag() > 0
+
+
+def test_exchange_buffer_plan_matches_oracle():
+    """communication_object::allocate: buffers per domain pair, fields in argument order with
+    alignof padding, tag offsets per pattern container — mixed f64/f32 fields (config 4 shape)."""
+    from ghex_amd import _ghx
+    ranks, gf, gl = H.cube_domains(5, (2, 2, 2))
+    types = [(8, 8), (4, 4), (8, 8), (4, 4), (8, 8)]
+    Hw = 3
+    for r in (0, 5):
+        pc = _regular_pattern_abi(ranks, gf, gl, (Hw,) * 6, (1, 1, 1), r)
+        opat = orc.regular_make_pattern(ranks, gf, gl, (Hw,) * 6, (1, 1, 1))
+        items, oitems = [], []
+        E = 5 + 2 * Hw
+        for k, (elem, align) in enumerate(types):
+            fd = _ghx.FieldDesc()
+            fd.dim, fd.elem_size = 3, elem
+            for d in range(3):
+                fd.layout[d] = 2 - d
+                fd.offsets[d] = Hw
+                fd.extents[d] = E
+            fd.byte_strides[0], fd.byte_strides[1], fd.byte_strides[2] = elem, elem * E, elem * E * E
+            fd.num_components, fd.has_components = 1, 0
+            it = _ghx.ExchangeItem()
+            it.pattern, it.local_index, it.kind, it.field = pc.handle, 0, 0, fd
+            it.align, it.tag_offset = align, 0
+            items.append(it)
+            oitems.append((k, r, opat[r][0], elem, align, 1, 0))
+        from ghex_amd.communication_object import _ExchangePlan
+        plan = _ExchangePlan(items)
+        for direction, receive in ((plan.send, False), (plan.recv, True)):
+            ob = orc.plan_buffers(oitems, receive)
+            assert [(b["pair"], b["rank"], b["tag"], b["size"]) for b in direction] == \
+                [(pair, b.rank, b.tag, b.size) for pair, b in ob.items()]
+        # 4-byte fields after 8-byte ones: the padding rule produced odd offsets somewhere?
+        sizes = [b["size"] for b in plan.send]
+        assert len(sizes) == 7
