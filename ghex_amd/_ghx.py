@@ -51,6 +51,7 @@ class ExchangeItem(ctypes.Structure):
 
 P = ctypes.POINTER
 _SIGS = {
+    "ghx_tune": (c_i32, [ctypes.c_char_p, c_i32]),
     "ghx_last_error": (ctypes.c_char_p, []),
     "ghx_version": (ctypes.c_char_p, []),
     "ghx_plan_create": (c_i32, [P(PackEntry), c_i32, c_i32, P(c_vp)]),

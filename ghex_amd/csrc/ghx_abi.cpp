@@ -260,6 +260,37 @@ const char* ghx_last_error(void) { return ghx::get_error(); }
 
 const char* ghx_version(void) { return "ghex_amd 0.1.0 (gfx950)"; }
 
+int ghx_tune(const char* key, int32_t value)
+{
+    return guarded([&] {
+        check_ptr(key, "key");
+        const std::string k(key);
+        if (k == "unroll")
+        {
+            if (value != 2 && value != 4 && value != 8) throw invalid("unroll must be 2, 4 or 8");
+            g_tune.unroll = value;
+        }
+        else if (k == "nt")
+        {
+            if (value < 0 || value > 2) throw invalid("nt must be 0, 1 or 2");
+            g_tune.nt = value;
+        }
+        else if (k == "grid_cap")
+        {
+            if (value < 0) throw invalid("grid_cap must be >= 0");
+            g_tune.grid_cap = value;
+        }
+        else if (k == "tile_bytes")
+        {
+            if (value < 1024 || uint32_t(value) > kMaxTileBytes || (value & (value - 1)))
+                throw invalid("tile_bytes must be a power of two in [1 KiB, 1 MiB]");
+            g_tune.tile_bytes = uint32_t(value);
+        }
+        else throw invalid("unknown tuning key: " + k);
+        return GHX_OK;
+    });
+}
+
 int ghx_plan_create(const ghx_pack_entry* entries, int32_t n_entries, int32_t direction,
                     ghx_plan** out)
 {

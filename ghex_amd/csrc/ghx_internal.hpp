@@ -17,9 +17,21 @@
 
 namespace ghx
 {
-// Bytes of buffer covered by one workgroup tile (256 threads x 4 vectors x 16 B).
+// Bytes of buffer covered by one workgroup tile (default 256 threads x 4 vectors x 16 B); the
+// tile size is a plan-time tuning knob bounded by kMaxTileBytes.
 constexpr uint32_t kTileBytes = 16384;
+constexpr uint32_t kMaxTileBytes = 1u << 20;
 constexpr int kBlock = 256;
+
+// Launch / planning knobs (ghx_tune). Defaults are the measured best.
+struct tuning
+{
+    int unroll = 4;                 // vectors in flight per lane per loop trip: 2, 4, 8
+    int nt = 0;                     // 0 default policy, 1 nt stores, 2 nt loads + stores
+    int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
+    uint32_t tile_bytes = kTileBytes;
+};
+extern tuning g_tune;
 
 // Unsigned 32-bit division by an invariant d via multiply-high (Granlund-Montgomery; the
 // round-up variant valid for every n < 2^32): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(m, n).
@@ -94,7 +106,7 @@ struct kargs
     const void* segs;
     const uint32_t* tile_seg;
     uint32_t n_tiles;
-    uint32_t pad;
+    uint32_t tile_bytes;
     uint64_t field_ptr[GHX_MAX_SLOTS];
     uint64_t buf_ptr[GHX_MAX_SLOTS];
 };

@@ -1,9 +1,9 @@
 // ghx_kernels.hip — gfx950 (CDNA4) pack / unpack kernels for the halo path.
 //
 // One launch covers every (field, iteration space, buffer) of a plan. Work is cut in the
-// BUFFER's byte space: a workgroup tile is kTileBytes (16 KiB) of one segment's buffer range,
-// so the buffer side is always a linear, fully coalesced 16 B/lane stream, and the field side
-// is linear within each contiguous row. Each lane decodes its buffer byte position into
+// BUFFER's byte space: a workgroup tile is tile_bytes (default 16 KiB) of one segment's buffer
+// range, so the buffer side is always a linear, fully coalesced 16 B/lane stream, and the field
+// side is linear within each contiguous row. Each lane decodes its buffer byte position into
 // (row, column) and the row into field coordinates with magic-number division, so no launch
 // depends on the shape of an iteration space: face, edge and corner spaces of all fields share
 // the one grid (the reference launches one kernel per iteration space per field,
@@ -13,12 +13,17 @@
 // Vector width per segment: the widest W in {16,8,4,2,1} bytes dividing the row length, the
 // row offsets/strides (planner) and the runtime base pointers (checked per tile here), so the
 // same plan is correct for any pointer alignment. No MFMA: this path is pure data movement.
+//
+// Variants (tuning, selected at launch): U = vectors in flight per lane per loop trip,
+// NT = cache policy (0 default, 1 non-temporal stores, 2 non-temporal loads and stores).
 #include <hip/hip_runtime.h>
 
 #include "ghx_internal.hpp"
 
 namespace ghx
 {
+tuning g_tune{};
+
 namespace
 {
 __device__ __forceinline__ uint32_t fastdiv(uint32_t n, magic_u32 m)
@@ -32,30 +37,42 @@ struct vec_t;
 template<>
 struct vec_t<16>
 {
-    using type = uint4;
+    using type = unsigned __attribute__((ext_vector_type(4)));
 };
 template<>
 struct vec_t<8>
 {
-    using type = uint2;
+    using type = unsigned __attribute__((ext_vector_type(2)));
 };
 template<>
 struct vec_t<4>
 {
-    using type = uint32_t;
+    using type = unsigned;
 };
 template<>
 struct vec_t<2>
 {
-    using type = uint16_t;
+    using type = unsigned short;
 };
 template<>
 struct vec_t<1>
 {
-    using type = uint8_t;
+    using type = unsigned char;
 };
 
-constexpr int kUnroll = 4;
+template<typename V, bool NTL>
+__device__ __forceinline__ V vload(const char* p)
+{
+    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+    else return *reinterpret_cast<const V*>(p);
+}
+
+template<typename V, bool NTS>
+__device__ __forceinline__ void vstore(char* p, V v)
+{
+    if constexpr (NTS) __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
+    else *reinterpret_cast<V*>(p) = v;
+}
 
 // field byte offset of segment-relative buffer position p (structured)
 __device__ __forceinline__ int64_t field_offset_s(const seg_s& s, uint32_t p)
@@ -72,81 +89,13 @@ __device__ __forceinline__ int64_t field_offset_s(const seg_s& s, uint32_t p)
            int64_t(c2) * s.stride[2] + int64_t(q2) * s.stride[3] + int64_t(col);
 }
 
-template<bool PACK, int W>
-__device__ __forceinline__ void copy_tile_s(const seg_s& s, char* __restrict__ field,
-                                            char* __restrict__ buf, uint32_t start, uint32_t end)
-{
-    using V = typename vec_t<W>::type;
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t base = start + tid * W; base < end; base += kUnroll * kBlock * W)
-    {
-        V v[kUnroll];
-        int64_t fo[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
-        {
-            const uint32_t p = base + u * kBlock * W;
-            if (p < end)
-            {
-                fo[u] = field_offset_s(s, p);
-                if (PACK) v[u] = *reinterpret_cast<const V*>(field + fo[u]);
-                else v[u] = *reinterpret_cast<const V*>(buf + p);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
-        {
-            const uint32_t p = base + u * kBlock * W;
-            if (p < end)
-            {
-                if (PACK) *reinterpret_cast<V*>(buf + p) = v[u];
-                else *reinterpret_cast<V*>(field + fo[u]) = v[u];
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ int ptr_wlog2(uint64_t p)
-{
-    // log2 of the largest power of two (<= 16) dividing p
-    return __builtin_ctzll(p | 16ull);
-}
-
-template<bool PACK>
-__global__ __launch_bounds__(kBlock) void k_structured(kargs a)
-{
-    const seg_s* __restrict__ segs = static_cast<const seg_s*>(a.segs);
-    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
-    {
-        const uint32_t si = a.tile_seg[t];
-        const seg_s s = segs[si];
-        const uint32_t start = (t - s.first_tile) * kTileBytes;
-        const uint32_t end = min(start + kTileBytes, s.bytes);
-        char* field = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
-        char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
-        int w = s.wlog2;
-        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
-        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
-        switch (w)
-        {
-            case 4: copy_tile_s<PACK, 16>(s, field, buf, start, end); break;
-            case 3: copy_tile_s<PACK, 8>(s, field, buf, start, end); break;
-            case 2: copy_tile_s<PACK, 4>(s, field, buf, start, end); break;
-            case 1: copy_tile_s<PACK, 2>(s, field, buf, start, end); break;
-            default: copy_tile_s<PACK, 1>(s, field, buf, start, end); break;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// unstructured: rows come from an index list
-// ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int64_t load_lid(const seg_u& s, uint32_t i)
 {
     if (s.lid64) return static_cast<const int64_t*>(s.lids)[i];
     return static_cast<const int32_t*>(s.lids)[i];
 }
 
+// field byte offset of segment-relative buffer position p (unstructured: rows from lids)
 __device__ __forceinline__ int64_t field_offset_u(const seg_u& s, uint32_t p)
 {
     const uint32_t row = fastdiv(p, s.mag_row);
@@ -170,55 +119,77 @@ __device__ __forceinline__ int64_t field_offset_u(const seg_u& s, uint32_t p)
     return load_lid(s, i) * s.index_stride_b + int64_t(l) * s.level_stride_b + int64_t(col);
 }
 
-template<bool PACK, int W>
-__device__ __forceinline__ void copy_tile_u(const seg_u& s, char* __restrict__ field,
-                                            char* __restrict__ buf, uint32_t start, uint32_t end)
+template<typename Seg>
+__device__ __forceinline__ int64_t field_offset(const Seg& s, uint32_t p);
+template<>
+__device__ __forceinline__ int64_t field_offset<seg_s>(const seg_s& s, uint32_t p)
+{
+    return field_offset_s(s, p);
+}
+template<>
+__device__ __forceinline__ int64_t field_offset<seg_u>(const seg_u& s, uint32_t p)
+{
+    return field_offset_u(s, p);
+}
+
+// Copy one tile [start, end) of a segment. Lane-linear in buffer space: lanes of a wave touch
+// consecutive W-byte vectors of the buffer; U independent vectors in flight per lane.
+template<bool PACK, int W, int U, int NT, typename Seg>
+__device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field,
+                                          char* __restrict__ buf, uint32_t start, uint32_t end)
 {
     using V = typename vec_t<W>::type;
+    constexpr bool NTL = NT >= 2;
+    constexpr bool NTS = NT >= 1;
     const uint32_t tid = threadIdx.x;
-    for (uint32_t base = start + tid * W; base < end; base += kUnroll * kBlock * W)
+    for (uint32_t base = start + tid * W; base < end; base += U * kBlock * W)
     {
-        V v[kUnroll];
-        int64_t fo[kUnroll];
+        V v[U];
+        int64_t fo[U];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
+        for (int u = 0; u < U; ++u)
         {
             const uint32_t p = base + u * kBlock * W;
-            if (p < end) fo[u] = field_offset_u(s, p);
+            if (p < end) fo[u] = field_offset<Seg>(s, p);
         }
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
+        for (int u = 0; u < U; ++u)
         {
             const uint32_t p = base + u * kBlock * W;
             if (p < end)
             {
-                if (PACK) v[u] = *reinterpret_cast<const V*>(field + fo[u]);
-                else v[u] = *reinterpret_cast<const V*>(buf + p);
+                if (PACK) v[u] = vload<V, NTL>(field + fo[u]);
+                else v[u] = vload<V, NTL>(buf + p);
             }
         }
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
+        for (int u = 0; u < U; ++u)
         {
             const uint32_t p = base + u * kBlock * W;
             if (p < end)
             {
-                if (PACK) *reinterpret_cast<V*>(buf + p) = v[u];
-                else *reinterpret_cast<V*>(field + fo[u]) = v[u];
+                if (PACK) vstore<V, NTS>(buf + p, v[u]);
+                else vstore<V, NTS>(field + fo[u], v[u]);
             }
         }
     }
 }
 
-template<bool PACK>
-__global__ __launch_bounds__(kBlock) void k_unstructured(kargs a)
+__device__ __forceinline__ int ptr_wlog2(uint64_t p)
 {
-    const seg_u* __restrict__ segs = static_cast<const seg_u*>(a.segs);
+    return __builtin_ctzll(p | 16ull);  // log2 of the largest power of two (<= 16) dividing p
+}
+
+template<bool PACK, int U, int NT, typename Seg>
+__global__ __launch_bounds__(kBlock) void k_copy(kargs a)
+{
+    const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
     for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
     {
         const uint32_t si = a.tile_seg[t];
-        const seg_u s = segs[si];
-        const uint32_t start = (t - s.first_tile) * kTileBytes;
-        const uint32_t end = min(start + kTileBytes, s.bytes);
+        const Seg s = segs[si];
+        const uint32_t start = (t - s.first_tile) * a.tile_bytes;
+        const uint32_t end = min(start + a.tile_bytes, s.bytes);
         char* field = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
         char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
         int w = s.wlog2;
@@ -226,28 +197,55 @@ __global__ __launch_bounds__(kBlock) void k_unstructured(kargs a)
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
         switch (w)
         {
-            case 4: copy_tile_u<PACK, 16>(s, field, buf, start, end); break;
-            case 3: copy_tile_u<PACK, 8>(s, field, buf, start, end); break;
-            case 2: copy_tile_u<PACK, 4>(s, field, buf, start, end); break;
-            case 1: copy_tile_u<PACK, 2>(s, field, buf, start, end); break;
-            default: copy_tile_u<PACK, 1>(s, field, buf, start, end); break;
+            case 4: copy_tile<PACK, 16, U, NT>(s, field, buf, start, end); break;
+            case 3: copy_tile<PACK, 8, U, NT>(s, field, buf, start, end); break;
+            case 2: copy_tile<PACK, 4, U, NT>(s, field, buf, start, end); break;
+            case 1: copy_tile<PACK, 2, U, NT>(s, field, buf, start, end); break;
+            default: copy_tile<PACK, 1, U, NT>(s, field, buf, start, end); break;
         }
     }
+}
+
+template<typename Seg, bool PACK>
+void launch_variant(const kargs& a, hipStream_t s, uint32_t grid)
+{
+    const int U = g_tune.unroll, NT = g_tune.nt;
+#define GHX_LAUNCH(UU, NN)                                                                   \
+    hipLaunchKernelGGL((k_copy<PACK, UU, NN, Seg>), dim3(grid), dim3(kBlock), 0, s, a)
+    if (U == 8)
+    {
+        if (NT == 2) GHX_LAUNCH(8, 2);
+        else if (NT == 1) GHX_LAUNCH(8, 1);
+        else GHX_LAUNCH(8, 0);
+    }
+    else if (U == 2)
+    {
+        if (NT == 2) GHX_LAUNCH(2, 2);
+        else if (NT == 1) GHX_LAUNCH(2, 1);
+        else GHX_LAUNCH(2, 0);
+    }
+    else
+    {
+        if (NT == 2) GHX_LAUNCH(4, 2);
+        else if (NT == 1) GHX_LAUNCH(4, 1);
+        else GHX_LAUNCH(4, 0);
+    }
+#undef GHX_LAUNCH
 }
 }  // namespace
 
 uint32_t grid_for_tiles(uint32_t n_tiles)
 {
-    // one tile per workgroup (hardware dispatch balances); grid-stride beyond 1M tiles
-    return n_tiles < (1u << 20) ? n_tiles : (1u << 20);
+    uint32_t cap = g_tune.grid_cap > 0 ? uint32_t(g_tune.grid_cap) : (1u << 20);
+    return n_tiles < cap ? n_tiles : cap;
 }
 
 int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid)
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (direction == 0) hipLaunchKernelGGL(k_structured<true>, dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL(k_structured<false>, dim3(grid), dim3(kBlock), 0, s, a);
+    if (direction == 0) launch_variant<seg_s, true>(a, s, grid);
+    else launch_variant<seg_s, false>(a, s, grid);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
     {
@@ -261,9 +259,8 @@ int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t gr
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (direction == 0)
-        hipLaunchKernelGGL(k_unstructured<true>, dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL(k_unstructured<false>, dim3(grid), dim3(kBlock), 0, s, a);
+    if (direction == 0) launch_variant<seg_u, true>(a, s, grid);
+    else launch_variant<seg_u, false>(a, s, grid);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
     {

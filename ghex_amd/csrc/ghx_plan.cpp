@@ -20,7 +20,7 @@ int wlog2_of(uint64_t v)  // log2 of the largest power of two <= 16 dividing v
     return std::min(4, ctz64(v));
 }
 
-uint32_t tiles_of(uint32_t bytes) { return (bytes + kTileBytes - 1) / kTileBytes; }
+uint32_t tiles_of(uint32_t bytes, uint32_t tb) { return (bytes + tb - 1) / tb; }
 
 bool have_device()
 {
@@ -158,7 +158,7 @@ uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, cons
     for (int k = 0; k + 1 < n_outer; ++k) rows_per_slowest *= oext[k];
     const int64_t slab = rows_per_slowest * L;  // bytes per unit of the slowest outer dim
     const int64_t nslow = n_outer > 0 ? oext[n_outer - 1] : 1;
-    const int64_t max_bytes = (int64_t(1) << 31) - kTileBytes;
+    const int64_t max_bytes = (int64_t(1) << 31) - kMaxTileBytes;
     int64_t chunk = n_outer > 0 ? std::max<int64_t>(1, max_bytes / slab) : 1;
     if (n_outer == 0 && L > max_bytes) throw invalid("segment too large");
     if (n_outer > 0 && slab > max_bytes) throw invalid("segment row block too large");
@@ -203,6 +203,7 @@ uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, cons
 
 splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(dir)
 {
+    tile_bytes = g_tune.tile_bytes;
     if (dir != 0 && dir != 1) throw invalid("direction must be 0 (pack) or 1 (unpack)");
     std::vector<seg_s> segs;
     for (int e = 0; e < n_entries; ++e)
@@ -225,7 +226,7 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
         segs[i].first_tile = uint32_t(tiles.size());
-        const uint32_t nt = tiles_of(segs[i].bytes);
+        const uint32_t nt = tiles_of(segs[i].bytes, tile_bytes);
         for (uint32_t t = 0; t < nt; ++t) tiles.push_back(i);
     }
     n_segments = int32_t(segs.size());
@@ -243,6 +244,7 @@ int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
     a.segs = dev.segs;
     a.tile_seg = dev.tiles;
     a.n_tiles = n_tiles;
+    a.tile_bytes = tile_bytes;
     for (int i = 0; i <= max_field_slot; ++i)
     {
         if (!fptr[i]) throw invalid("null field pointer");
@@ -261,6 +263,7 @@ int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
 // ---------------------------------------------------------------------------------------------
 uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction(dir)
 {
+    tile_bytes = g_tune.tile_bytes;
     if (dir != 0 && dir != 1) throw invalid("direction must be 0 (pack) or 1 (unpack)");
     std::vector<seg_u> segs;
     // all index lists in one device allocation: int32 where they fit
@@ -288,7 +291,7 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         if (en.n_lids == 0) continue;
         const int64_t elem = d.elem_size;
         const int64_t total = en.n_lids * d.levels * elem;
-        if (total >= (int64_t(1) << 31) - kTileBytes || en.n_lids >= (int64_t(1) << 32))
+        if (total >= (int64_t(1) << 31) - kMaxTileBytes || en.n_lids >= (int64_t(1) << 32))
             throw invalid("unstructured segment too large");
         bool wide = false;
         for (int64_t i = 0; i < en.n_lids; ++i)
@@ -341,7 +344,7 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
         segs[i].first_tile = uint32_t(tiles.size());
-        const uint32_t nt = tiles_of(segs[i].bytes);
+        const uint32_t nt = tiles_of(segs[i].bytes, tile_bytes);
         for (uint32_t t = 0; t < nt; ++t) tiles.push_back(i);
     }
     n_segments = int32_t(segs.size());
@@ -378,6 +381,7 @@ int uplan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
     a.segs = dev.segs;
     a.tile_seg = dev.tiles;
     a.n_tiles = n_tiles;
+    a.tile_bytes = tile_bytes;
     for (int i = 0; i <= max_field_slot; ++i)
     {
         if (!fptr[i]) throw invalid("null field pointer");

@@ -41,6 +41,7 @@ struct splan
     uint64_t bytes = 0;
     int32_t n_segments = 0;
     uint32_t n_tiles = 0;
+    uint32_t tile_bytes = kTileBytes;
     int max_field_slot = -1, max_buf_slot = -1;
     std::vector<seg_s> host_segs;
     device_tables dev;
@@ -55,6 +56,7 @@ struct uplan
     uint64_t bytes = 0;
     int32_t n_segments = 0;
     uint32_t n_tiles = 0;
+    uint32_t tile_bytes = kTileBytes;
     int max_field_slot = -1, max_buf_slot = -1;
     device_tables dev;
     uplan(const ghx_upack_entry* entries, int n_entries, int direction);

@@ -43,6 +43,14 @@ typedef void* ghx_stream;
 #define GHX_MAX_DIM 4     /* 3 spatial dims + 1 component axis (bindings/python/src/_pyghex/structured/types.hpp:31-63) */
 #define GHX_MAX_SLOTS 64  /* field / buffer pointer slots per plan execution */
 
+/* Process-wide tuning knobs (development / benchmarking; defaults are the measured best):
+ * "unroll" (2|4|8 vectors in flight per lane), "nt" (0 default cache policy, 1 non-temporal
+ * stores, 2 non-temporal loads and stores), "grid_cap" (max workgroups, 0 = one per tile),
+ * "tile_bytes" (buffer bytes per workgroup tile; applies to plans created afterwards).
+ * No reference counterpart (the reference hard-codes block_dim=128, 1 element per thread:
+ * include/ghex/structured/pack_kernels.hpp:211-214). */
+int ghx_tune(const char* key, int32_t value);
+
 /* Last error message of the calling thread ("" if none). */
 const char* ghx_last_error(void);
 /* Library version string and the offload target it was compiled for ("gfx950"). */

@@ -345,7 +345,7 @@ def structured_pack(f: FieldSpec, buffer: np.ndarray, boxes: Sequence[ISPair], b
     bs, bs_p = _i64(f.byte_strides)
     off, off_p = _i32(f.offsets)
     bx, bx_p = _i32(expand_boxes(f, boxes))
-    assert buffer.flags.c_contiguous and f.data.flags.c_contiguous or f.data.flags.f_contiguous
+    assert buffer.flags.c_contiguous  # the field may be any strided view: byte_strides rule
     return L.orc_structured_pack(f.data.ctypes.data, buffer.ctypes.data + byte_offset, f.D, f.elem,
                                  lay_p, bs_p, off_p, bx_p, len(boxes), 1 if elementwise else 0)
 

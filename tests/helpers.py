@@ -91,7 +91,7 @@ def linear_index_field(dom, N, H, g_last, dtype=np.float64, layout=(2, 1, 0), se
     E = N + 2 * H
     order = sorted(range(3), key=lambda d: layout[d])  # slowest ... fastest dim
     shape = tuple(E for _ in order)
-    a = np.full(shape, -1, dtype=dtype)
+    a = np.full(shape, -1).astype(dtype)  # -1 sentinel (wraps for unsigned types)
     gx, gy, gz = g_last[0] + 1, g_last[1] + 1, g_last[2] + 1
     idx = np.meshgrid(*[np.arange(N) for _ in range(3)], indexing="ij")  # idx[k] over memory axes
     coords = [None, None, None]
