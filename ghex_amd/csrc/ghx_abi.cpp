@@ -272,8 +272,24 @@ int ghx_tune(const char* key, int32_t value)
         }
         else if (k == "nt")
         {
-            if (value < 0 || value > 2) throw invalid("nt must be 0, 1 or 2");
+            if (value < 0 || value > 3) throw invalid("nt must be 0, 1, 2 or 3");
             g_tune.nt = value;
+        }
+        else if (k == "order")
+        {
+            if (value < 0 || value > 2) throw invalid("order must be 0, 1 or 2");
+            g_tune.order = value;
+        }
+        else if (k == "small_row_bytes")
+        {
+            if (value < 1) throw invalid("small_row_bytes must be >= 1");
+            g_tune.small_row_bytes = uint32_t(value);
+        }
+        else if (k == "small_tile_bytes")
+        {
+            if (value < 1024 || uint32_t(value) > kMaxTileBytes || (value & (value - 1)))
+                throw invalid("small_tile_bytes must be a power of two in [1 KiB, 1 MiB]");
+            g_tune.small_tile_bytes = uint32_t(value);
         }
         else if (k == "grid_cap")
         {

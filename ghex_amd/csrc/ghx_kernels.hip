@@ -139,8 +139,8 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
                                           char* __restrict__ buf, uint32_t start, uint32_t end)
 {
     using V = typename vec_t<W>::type;
-    constexpr bool NTL = NT >= 2;
-    constexpr bool NTS = NT >= 1;
+    constexpr bool NTL = NT >= 2;             // 2, 3: non-temporal loads
+    constexpr bool NTS = NT == 1 || NT == 2;  // 1, 2: non-temporal stores
     const uint32_t tid = threadIdx.x;
     for (uint32_t base = start + tid * W; base < end; base += U * kBlock * W)
     {
@@ -186,10 +186,11 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
     const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
     for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
     {
-        const uint32_t si = a.tile_seg[t];
+        const uint32_t si = a.tile_seg[2 * t];
+        const uint32_t ti = a.tile_seg[2 * t + 1];
         const Seg s = segs[si];
-        const uint32_t start = (t - s.first_tile) * a.tile_bytes;
-        const uint32_t end = min(start + a.tile_bytes, s.bytes);
+        const uint32_t start = ti << s.tile_shift;
+        const uint32_t end = min(start + (1u << s.tile_shift), s.bytes);
         char* field = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
         char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
         int w = s.wlog2;
@@ -206,31 +207,24 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
     }
 }
 
+template<typename Seg, bool PACK, int U>
+void launch_nt(const kargs& a, hipStream_t s, uint32_t grid)
+{
+    switch (g_tune.nt)
+    {
+        case 1: hipLaunchKernelGGL((k_copy<PACK, U, 1, Seg>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_copy<PACK, U, 2, Seg>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_copy<PACK, U, 3, Seg>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_copy<PACK, U, 0, Seg>), dim3(grid), dim3(kBlock), 0, s, a); break;
+    }
+}
+
 template<typename Seg, bool PACK>
 void launch_variant(const kargs& a, hipStream_t s, uint32_t grid)
 {
-    const int U = g_tune.unroll, NT = g_tune.nt;
-#define GHX_LAUNCH(UU, NN)                                                                   \
-    hipLaunchKernelGGL((k_copy<PACK, UU, NN, Seg>), dim3(grid), dim3(kBlock), 0, s, a)
-    if (U == 8)
-    {
-        if (NT == 2) GHX_LAUNCH(8, 2);
-        else if (NT == 1) GHX_LAUNCH(8, 1);
-        else GHX_LAUNCH(8, 0);
-    }
-    else if (U == 2)
-    {
-        if (NT == 2) GHX_LAUNCH(2, 2);
-        else if (NT == 1) GHX_LAUNCH(2, 1);
-        else GHX_LAUNCH(2, 0);
-    }
-    else
-    {
-        if (NT == 2) GHX_LAUNCH(4, 2);
-        else if (NT == 1) GHX_LAUNCH(4, 1);
-        else GHX_LAUNCH(4, 0);
-    }
-#undef GHX_LAUNCH
+    if (g_tune.unroll == 8) launch_nt<Seg, PACK, 8>(a, s, grid);
+    else if (g_tune.unroll == 2) launch_nt<Seg, PACK, 2>(a, s, grid);
+    else launch_nt<Seg, PACK, 4>(a, s, grid);
 }
 }  // namespace
 

@@ -22,6 +22,58 @@ int wlog2_of(uint64_t v)  // log2 of the largest power of two <= 16 dividing v
 
 uint32_t tiles_of(uint32_t bytes, uint32_t tb) { return (bytes + tb - 1) / tb; }
 
+int log2u(uint32_t v)
+{
+    int l = 0;
+    while ((1u << l) < v) ++l;
+    return l;
+}
+
+// Tile table: per tile {segment, tile index within the segment}. Segments with short rows
+// (request-bound: one memory request per row) may use a different tile size from streaming
+// segments; the dispatch order of tiles is a tuning knob (hardware dispatches in blockIdx order).
+template<typename Seg>
+std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
+{
+    std::vector<std::vector<uint32_t>> per(segs.size());
+    for (uint32_t i = 0; i < segs.size(); ++i)
+    {
+        const bool small = segs[i].row_bytes < g_tune.small_row_bytes;
+        const uint32_t tb = small ? g_tune.small_tile_bytes : g_tune.tile_bytes;
+        segs[i].tile_shift = uint8_t(log2u(tb));
+        segs[i].first_tile = 0;
+        const uint32_t nt = tiles_of(segs[i].bytes, tb);
+        for (uint32_t t = 0; t < nt; ++t) per[i].push_back(t);
+    }
+    std::vector<uint32_t> out;
+    auto emit = [&](uint32_t i, uint32_t t) {
+        out.push_back(i);
+        out.push_back(t);
+    };
+    if (g_tune.order == 2)
+    {
+        // round-robin over segments
+        size_t maxn = 0;
+        for (auto& v : per) maxn = std::max(maxn, v.size());
+        for (size_t k = 0; k < maxn; ++k)
+            for (uint32_t i = 0; i < segs.size(); ++i)
+                if (k < per[i].size()) emit(i, per[i][k]);
+    }
+    else
+    {
+        std::vector<uint32_t> idx(segs.size());
+        for (uint32_t i = 0; i < segs.size(); ++i) idx[i] = i;
+        if (g_tune.order == 1)
+            std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+                return (segs[a].row_bytes < g_tune.small_row_bytes) >
+                       (segs[b].row_bytes < g_tune.small_row_bytes);
+            });
+        for (uint32_t i : idx)
+            for (uint32_t t : per[i]) emit(i, t);
+    }
+    return out;
+}
+
 bool have_device()
 {
     int n = 0;
@@ -222,15 +274,9 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
                                     uint16_t(en.buffer_slot), off);
         bytes += off - en.buffer_offset;
     }
-    std::vector<uint32_t> tiles;
-    for (uint32_t i = 0; i < segs.size(); ++i)
-    {
-        segs[i].first_tile = uint32_t(tiles.size());
-        const uint32_t nt = tiles_of(segs[i].bytes, tile_bytes);
-        for (uint32_t t = 0; t < nt; ++t) tiles.push_back(i);
-    }
+    std::vector<uint32_t> tiles = build_tiles(segs);
     n_segments = int32_t(segs.size());
-    n_tiles = uint32_t(tiles.size());
+    n_tiles = uint32_t(tiles.size() / 2);
     host_segs = segs;
     upload(dev, segs, tiles);
 }
@@ -244,7 +290,6 @@ int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
     a.segs = dev.segs;
     a.tile_seg = dev.tiles;
     a.n_tiles = n_tiles;
-    a.tile_bytes = tile_bytes;
     for (int i = 0; i <= max_field_slot; ++i)
     {
         if (!fptr[i]) throw invalid("null field pointer");
@@ -340,15 +385,9 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         segs.push_back(s);
         bytes += uint64_t(total);
     }
-    std::vector<uint32_t> tiles;
-    for (uint32_t i = 0; i < segs.size(); ++i)
-    {
-        segs[i].first_tile = uint32_t(tiles.size());
-        const uint32_t nt = tiles_of(segs[i].bytes, tile_bytes);
-        for (uint32_t t = 0; t < nt; ++t) tiles.push_back(i);
-    }
+    std::vector<uint32_t> tiles = build_tiles(segs);
     n_segments = int32_t(segs.size());
-    n_tiles = uint32_t(tiles.size());
+    n_tiles = uint32_t(tiles.size() / 2);
     if (!segs.empty() && have_device())
     {
         std::vector<unsigned char> host(lid_bytes);
@@ -381,7 +420,6 @@ int uplan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
     a.segs = dev.segs;
     a.tile_seg = dev.tiles;
     a.n_tiles = n_tiles;
-    a.tile_bytes = tile_bytes;
     for (int i = 0; i <= max_field_slot; ++i)
     {
         if (!fptr[i]) throw invalid("null field pointer");
