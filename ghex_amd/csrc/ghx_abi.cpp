@@ -285,11 +285,10 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 1) throw invalid("small_row_bytes must be >= 1");
             g_tune.small_row_bytes = uint32_t(value);
         }
-        else if (k == "small_tile_bytes")
+        else if (k == "small_tile_rows")
         {
-            if (value < 1024 || uint32_t(value) > kMaxTileBytes || (value & (value - 1)))
-                throw invalid("small_tile_bytes must be a power of two in [1 KiB, 1 MiB]");
-            g_tune.small_tile_bytes = uint32_t(value);
+            if (value < 64 || value > (1 << 16)) throw invalid("small_tile_rows must be in [64, 65536]");
+            g_tune.small_tile_rows = uint32_t(value);
         }
         else if (k == "grid_cap")
         {

@@ -29,11 +29,11 @@ struct tuning
     int unroll = 4;                 // vectors in flight per lane per loop trip: 2, 4, 8
     int nt = 0;                     // 0 default, 1 nt stores, 2 nt loads + stores, 3 nt loads
     int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
-    uint32_t tile_bytes = kTileBytes;        // tile of segments with long rows
-    uint32_t small_tile_bytes = kTileBytes;  // tile of segments with short rows
-    uint32_t small_row_bytes = 64;           // rows shorter than this are "short"
-    int order = 0;                  // tile dispatch order: 0 segment order, 1 short-row segments
-                                    // first, 2 round-robin over segments
+    uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
+    uint32_t small_tile_rows = 4096;   // rows per tile of segments with short rows
+    uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
+    int order = 1;                     // tile dispatch order: 0 segment order, 1 short-row
+                                       // segments first, 2 round-robin over segments
 };
 extern tuning g_tune;
 
@@ -75,8 +75,9 @@ struct alignas(16) seg_s
     uint16_t buf_slot;
     uint8_t wlog2;        // log2 of the widest vector (<= 16 B) that divides L, offsets, strides
     uint8_t n_outer;
-    uint8_t tile_shift;   // log2 of this segment's tile size in bytes
-    uint8_t pad[13];
+    uint8_t pad1[2];
+    uint32_t tile_bytes;  // this segment's tile size (a multiple of the row length or 16 KiB)
+    uint8_t pad[8];
 };
 static_assert(sizeof(seg_s) == 128, "seg_s layout");
 
@@ -101,8 +102,9 @@ struct alignas(16) seg_u
                                // 1: rows (i,l) i-major (levels_first, strided levels)
                                // 2: rows (l,i) l-major (levels_last)
     uint8_t lid64;
-    uint8_t tile_shift;
-    uint8_t pad[12];
+    uint8_t pad1;
+    uint32_t tile_bytes;
+    uint8_t pad[8];
 };
 static_assert(sizeof(seg_u) == 96, "seg_u layout");
 

@@ -189,8 +189,8 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         const uint32_t si = a.tile_seg[2 * t];
         const uint32_t ti = a.tile_seg[2 * t + 1];
         const Seg s = segs[si];
-        const uint32_t start = ti << s.tile_shift;
-        const uint32_t end = min(start + (1u << s.tile_shift), s.bytes);
+        const uint32_t start = ti * s.tile_bytes;
+        const uint32_t end = min(start + s.tile_bytes, s.bytes);
         char* field = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
         char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
         int w = s.wlog2;

@@ -22,13 +22,6 @@ int wlog2_of(uint64_t v)  // log2 of the largest power of two <= 16 dividing v
 
 uint32_t tiles_of(uint32_t bytes, uint32_t tb) { return (bytes + tb - 1) / tb; }
 
-int log2u(uint32_t v)
-{
-    int l = 0;
-    while ((1u << l) < v) ++l;
-    return l;
-}
-
 // Tile table: per tile {segment, tile index within the segment}. Segments with short rows
 // (request-bound: one memory request per row) may use a different tile size from streaming
 // segments; the dispatch order of tiles is a tuning knob (hardware dispatches in blockIdx order).
@@ -39,8 +32,14 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
         const bool small = segs[i].row_bytes < g_tune.small_row_bytes;
-        const uint32_t tb = small ? g_tune.small_tile_bytes : g_tune.tile_bytes;
-        segs[i].tile_shift = uint8_t(log2u(tb));
+        uint32_t tb = g_tune.tile_bytes;
+        if (small)
+        {
+            const uint64_t want = uint64_t(g_tune.small_tile_rows) * segs[i].row_bytes;
+            tb = uint32_t(std::max<uint64_t>(segs[i].row_bytes, std::min<uint64_t>(want, kMaxTileBytes)));
+            tb -= tb % segs[i].row_bytes;  // whole rows per tile
+        }
+        segs[i].tile_bytes = tb;
         segs[i].first_tile = 0;
         const uint32_t nt = tiles_of(segs[i].bytes, tb);
         for (uint32_t t = 0; t < nt; ++t) per[i].push_back(t);

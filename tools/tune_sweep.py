@@ -11,8 +11,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULTS = dict(unroll=4, nt=0, grid_cap=0, tile_bytes=16384, small_tile_bytes=16384,
-                small_row_bytes=64, order=0)
+DEFAULTS = dict(unroll=4, nt=0, grid_cap=0, tile_bytes=16384, small_tile_rows=4096,
+                small_row_bytes=64, order=1)
 
 
 def main():
