@@ -280,6 +280,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 2) throw invalid("order must be 0, 1 or 2");
             g_tune.order = value;
         }
+        else if (k == "pair")
+        {
+            if (value < 0 || value > 1) throw invalid("pair must be 0 or 1");
+            g_tune.pair = value;
+        }
         else if (k == "small_row_bytes")
         {
             if (value < 1) throw invalid("small_row_bytes must be >= 1");

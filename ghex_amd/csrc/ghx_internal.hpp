@@ -34,6 +34,9 @@ struct tuning
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     int order = 1;                     // tile dispatch order: 0 segment order, 1 short-row
                                        // segments first, 2 round-robin over segments
+    int pair = 1;                      // pair short-row segments whose rows interleave in
+                                       // memory (the +x face of row y and the -x face of row
+                                       // y+1 share a cache line): one lane moves both
 };
 extern tuning g_tune;
 
@@ -77,7 +80,8 @@ struct alignas(16) seg_s
     uint8_t n_outer;
     uint8_t pad1[2];
     uint32_t tile_bytes;  // this segment's tile size (a multiple of the row length or 16 KiB)
-    uint8_t pad[8];
+    int32_t partner;      // paired segment (row r here travels with its row r-1), or -1
+    uint8_t pad[4];
 };
 static_assert(sizeof(seg_s) == 128, "seg_s layout");
 

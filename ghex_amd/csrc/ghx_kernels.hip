@@ -175,6 +175,107 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
     }
 }
 
+// Paired segments (planner: pair_segments): lane moves row r of the primary and row r-1 of the
+// partner, whose field pieces share a cache line; both buffer streams stay lane-linear.
+template<bool PACK, int W, int U, int NT>
+__device__ __forceinline__ void copy_tile_pair(const seg_s& s, const seg_s& q,
+                                               char* __restrict__ field, char* __restrict__ buf,
+                                               char* __restrict__ qbuf, uint32_t start,
+                                               uint32_t end)
+{
+    using V = typename vec_t<W>::type;
+    constexpr bool NTL = NT >= 2;
+    constexpr bool NTS = NT == 1 || NT == 2;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t L = s.row_bytes;
+    for (uint32_t base = start + tid * W; base < end; base += U * kBlock * W)
+    {
+        V v[U], w[U];
+        int64_t fo[U], fq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                fo[u] = field_offset_s(s, p);
+                if (p >= L) fq[u] = field_offset_s(q, p - L);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                if (PACK)
+                {
+                    v[u] = vload<V, NTL>(field + fo[u]);
+                    if (p >= L) w[u] = vload<V, NTL>(field + fq[u]);
+                }
+                else
+                {
+                    v[u] = vload<V, NTL>(buf + p);
+                    if (p >= L) w[u] = vload<V, NTL>(qbuf + (p - L));
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                if (PACK)
+                {
+                    vstore<V, NTS>(buf + p, v[u]);
+                    if (p >= L) vstore<V, NTS>(qbuf + (p - L), w[u]);
+                }
+                else
+                {
+                    vstore<V, NTS>(field + fo[u], v[u]);
+                    if (p >= L) vstore<V, NTS>(field + fq[u], w[u]);
+                }
+            }
+        }
+    }
+}
+
+template<bool PACK, int U, int NT>
+__device__ __forceinline__ void dispatch_pair(const seg_s& s, const seg_s& q, char* field,
+                                              char* buf, char* qbuf, uint32_t start, uint32_t end,
+                                              int w)
+{
+    switch (w)
+    {
+        case 4: copy_tile_pair<PACK, 16, U, NT>(s, q, field, buf, qbuf, start, end); break;
+        case 3: copy_tile_pair<PACK, 8, U, NT>(s, q, field, buf, qbuf, start, end); break;
+        case 2: copy_tile_pair<PACK, 4, U, NT>(s, q, field, buf, qbuf, start, end); break;
+        case 1: copy_tile_pair<PACK, 2, U, NT>(s, q, field, buf, qbuf, start, end); break;
+        default: copy_tile_pair<PACK, 1, U, NT>(s, q, field, buf, qbuf, start, end); break;
+    }
+}
+
+template<bool PACK, int U, int NT, typename Seg>
+__device__ __forceinline__ bool try_pair(const Seg&, const Seg*, const kargs&, char*, char*,
+                                         uint32_t, uint32_t, int)
+{
+    return false;
+}
+
+template<bool PACK, int U, int NT>
+__device__ __forceinline__ bool try_pair(const seg_s& s, const seg_s* segs, const kargs& a,
+                                         char* field, char* buf, uint32_t start, uint32_t end,
+                                         int w)
+{
+    if (s.partner < 0) return false;
+    const seg_s q = segs[s.partner];
+    char* qbuf = reinterpret_cast<char*>(a.buf_ptr[q.buf_slot]) + q.buf_off;
+    w = min(w, int(__builtin_ctzll(reinterpret_cast<uint64_t>(qbuf) | 16ull)));
+    dispatch_pair<PACK, U, NT>(s, q, field, buf, qbuf, start, end, w);
+    return true;
+}
+
 __device__ __forceinline__ int ptr_wlog2(uint64_t p)
 {
     return __builtin_ctzll(p | 16ull);  // log2 of the largest power of two (<= 16) dividing p
@@ -196,6 +297,7 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         int w = s.wlog2;
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+        if (try_pair<PACK, U, NT>(s, segs, a, field, buf, start, end, w)) continue;
         switch (w)
         {
             case 4: copy_tile<PACK, 16, U, NT>(s, field, buf, start, end); break;

@@ -26,11 +26,12 @@ uint32_t tiles_of(uint32_t bytes, uint32_t tb) { return (bytes + tb - 1) / tb; }
 // (request-bound: one memory request per row) may use a different tile size from streaming
 // segments; the dispatch order of tiles is a tuning knob (hardware dispatches in blockIdx order).
 template<typename Seg>
-std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
+std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char>* skip = nullptr)
 {
     std::vector<std::vector<uint32_t>> per(segs.size());
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
+        if (skip && (*skip)[i]) continue;  // moved by its pair partner's tiles
         const bool small = segs[i].row_bytes < g_tune.small_row_bytes;
         uint32_t tb = g_tune.tile_bytes;
         if (small)
@@ -71,6 +72,73 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
             for (uint32_t t : per[i]) emit(i, t);
     }
     return out;
+}
+
+int wlog2_seg(const seg_s& s)
+{
+    int w = wlog2_of(uint64_t(s.row_bytes));
+    w = std::min(w, wlog2_of(uint64_t(s.field_off)));
+    w = std::min(w, wlog2_of(s.buf_off));
+    for (int k = 0; k < s.n_outer; ++k)
+        if (s.ext[k] > 1)
+            w = std::min(w, wlog2_of(uint64_t(s.stride[k] < 0 ? -s.stride[k] : s.stride[k])));
+    return w;
+}
+
+// Pair short-row segments of one field whose rows interleave in memory: row r of the primary P
+// and row r-1 of the partner Q lie within one 128 B line when
+// 0 < P.field_off + P.stride[0] - Q.field_off < 128 (for unpadded rows of a structured field:
+// the +x face of row y ends 48 B before the -x face of row y+1 starts at H=2). One lane then
+// moves both pieces, so their shared line is requested once instead of twice. Q's last row has
+// no primary row after it and becomes a 1-row tail segment. Returns the consumed mask.
+std::vector<char> pair_segments(std::vector<seg_s>& segs)
+{
+    std::vector<char> consumed(segs.size(), 0);
+    const size_t n0 = segs.size();
+    for (size_t i = 0; i < n0; ++i)
+    {
+        auto& p = segs[i];
+        if (consumed[i] || p.partner >= 0 || p.row_bytes >= g_tune.small_row_bytes || p.n_outer < 1)
+            continue;
+        for (size_t j = 0; j < n0; ++j)
+        {
+            if (j == i || consumed[j] || segs[j].partner >= 0) continue;
+            const auto& q = segs[j];
+            bool same = q.field_slot == p.field_slot && q.row_bytes == p.row_bytes &&
+                        q.n_outer == p.n_outer && q.bytes == p.bytes && q.wlog2 == p.wlog2;
+            for (int k = 0; same && k < 4; ++k)
+                same = q.ext[k] == p.ext[k] && q.stride[k] == p.stride[k];
+            if (!same || p.bytes / p.row_bytes < 2) continue;
+            const int64_t d = p.field_off + p.stride[0] - q.field_off;
+            if (d <= 0 || d >= 128 || d < int64_t(p.row_bytes)) continue;  // disjoint, one line
+            bool taken = false;
+            for (size_t k = 0; k < n0 && !taken; ++k) taken = segs[k].partner == int32_t(j);
+            if (taken) continue;
+            p.partner = int32_t(j);
+            consumed[j] = 1;
+            // tail: Q's last row (r = R-1)
+            seg_s t = q;
+            int64_t off = 0;
+            for (int k = 0; k < 4; ++k) off += int64_t(q.ext[k] - 1) * q.stride[k];
+            const uint32_t R = q.bytes / q.row_bytes;
+            t.field_off = q.field_off + off;
+            t.buf_off = q.buf_off + uint64_t(R - 1) * q.row_bytes;
+            for (int k = 0; k < 4; ++k)
+            {
+                t.ext[k] = 1;
+                t.stride[k] = 0;
+            }
+            for (int k = 0; k < 3; ++k) t.mag_ext[k] = make_magic(1);
+            t.n_outer = 0;
+            t.bytes = q.row_bytes;
+            t.partner = -1;
+            t.wlog2 = uint8_t(wlog2_seg(t));
+            segs.push_back(t);
+            consumed.push_back(0);
+            break;
+        }
+    }
+    return consumed;
 }
 
 bool have_device()
@@ -217,6 +285,7 @@ uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, cons
     {
         const int64_t cnt = std::min(chunk, nslow - s0);
         seg_s s{};
+        s.partner = -1;
         s.field_slot = field_slot;
         s.buf_slot = buf_slot;
         s.row_bytes = uint32_t(L);
@@ -273,7 +342,9 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
                                     uint16_t(en.buffer_slot), off);
         bytes += off - en.buffer_offset;
     }
-    std::vector<uint32_t> tiles = build_tiles(segs);
+    std::vector<char> consumed;
+    if (g_tune.pair) consumed = pair_segments(segs);
+    std::vector<uint32_t> tiles = build_tiles(segs, g_tune.pair ? &consumed : nullptr);
     n_segments = int32_t(segs.size());
     n_tiles = uint32_t(tiles.size() / 2);
     host_segs = segs;
