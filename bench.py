@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true")
+    p.add_argument("--tune", default="", help="developer: ghx_tune key=value,... before planning")
     return p.parse_args()
 
 
@@ -65,6 +66,9 @@ def main():
     from ghex_amd import _ghx
     from ghex_amd.structured import regular as R
     ghex_amd.native_library()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _ghx.call("ghx_tune", k.encode(), int(v))
 
     N, Hw = args.N, args.halo
     E = N + 2 * Hw
