@@ -34,9 +34,11 @@ struct tuning
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     int order = 1;                     // tile dispatch order: 0 segment order, 1 short-row
                                        // segments first, 2 round-robin over segments
-    int pair = 1;                      // pair short-row segments whose rows interleave in
+    int pair = 0;                      // pair short-row segments whose rows interleave in
                                        // memory (the +x face of row y and the -x face of row
-                                       // y+1 share a cache line): one lane moves both
+                                       // y+1 share a cache line): one lane moves both. Off by
+                                       // default: with short-row-first dispatch the L2 already
+                                       // merges the shared-line misses (same TCC_EA0_RDREQ)
 };
 extern tuning g_tune;
 
