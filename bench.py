@@ -186,20 +186,10 @@ def main():
     }
 
     # ---- per-kernel HIP-event durations (dominant kernel roofline) ----------------------------
-    kk = min(K, 100)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(kk)]
-    torch.cuda.synchronize(dev)
-    for i in range(kk):
-        s = torch.cuda.current_stream(dev).cuda_stream
-        ev[i][0].record(stream)
-        pack(s)
-        ev[i][1].record(stream)
-        ev[i][2].record(stream)
-        unpack(s)
-        ev[i][3].record(stream)
-    torch.cuda.synchronize(dev)
-    t_pack = sum(e[0].elapsed_time(e[1]) for e in ev) / kk * 1e-3
-    t_unpack = sum(e[2].elapsed_time(e[3]) for e in ev) / kk * 1e-3
+    # Differential method (removes the fixed cost of the events themselves): hipGraphs of M steps,
+    # of M steps + one pack, and of M steps + one pack + one unpack, replayed in interleaved
+    # rounds; pack = T1 - T0, unpack = T2 - T1 (each includes its dependent-launch boundary).
+    t_pack, t_unpack = kernel_durations(torch, dev, stream, pack, unpack)
     launch_bytes = 2 * n_halo * 8
     dom_name, dom_t = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
     achieved = launch_bytes / dom_t / 1e9
@@ -257,6 +247,44 @@ def main():
     if world > 1:
         dist.barrier(device_ids=[local])
         dist.destroy_process_group()
+
+
+def kernel_durations(torch, dev, stream, pack, unpack, M=10, rounds=15):
+    def capture(extra):
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            s = side.cuda_stream
+            pack(s)
+            unpack(s)
+        stream.wait_stream(side)
+        with torch.cuda.graph(g):
+            s = torch.cuda.current_stream(dev).cuda_stream
+            for _ in range(M):
+                pack(s)
+                unpack(s)
+            if extra >= 1:
+                pack(s)
+            if extra >= 2:
+                unpack(s)
+        return g
+
+    graphs = [capture(e) for e in range(3)]
+    times = [[], [], []]
+    for g in graphs:
+        g.replay()
+    torch.cuda.synchronize(dev)
+    for _ in range(rounds):
+        for i, g in enumerate(graphs):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            g.replay()
+            e1.record(stream)
+            e1.synchronize()
+            times[i].append(e0.elapsed_time(e1) * 1e-3)
+    med = [sorted(t)[len(t) // 2] for t in times]
+    return med[1] - med[0], med[2] - med[1]
 
 
 def cpu_baseline(N, Hw, seconds):

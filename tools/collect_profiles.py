@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Copy the judged rocprofv3 summaries of a round from gpurun_out/prof_<round>/ into profiles/:
+
+  profiles/<round>_bench_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `python3 bench.py`
+  profiles/<round>_h{1,3}_kernel_stats.csv  the same at halo 1 / 3
+  profiles/<round>_pmc.json                 per-kernel counters + corrected HBM bytes per launch
+  profiles/pmc_traffic.json                 what bench.py reads for roofline.traffic
+  profiles/<round>_bench.json               the bench JSON line printed under the profiler
+"""
+import json
+import os
+import shutil
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+from parse_pmc import main as parse_pmc  # noqa: E402
+
+
+def main(rn):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{rn}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "bench", "kt_kernel_stats.csv"),
+                os.path.join(dst, f"{rn}_bench_kernel_stats.csv"))
+    for h in (1, 3):
+        p = os.path.join(src, f"h{h}", "kt_kernel_stats.csv")
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, f"{rn}_h{h}_kernel_stats.csv"))
+    line = [l for l in open(os.path.join(src, "bench.log")) if l.startswith("{")]
+    if line:
+        with open(os.path.join(dst, f"{rn}_bench.json"), "w") as fh:
+            fh.write(line[-1])
+    pmc, traffic = {}, {}
+    for h in (1, 2, 3):
+        d = os.path.join(src, f"pmc_h{h}")
+        if os.path.isdir(d):
+            r = parse_pmc(d)
+            pmc[f"N512_H{h}"] = r
+            traffic[f"N512_H{h}"] = {k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"]}
+                                     for k, v in r.items()}
+    with open(os.path.join(dst, f"{rn}_pmc.json"), "w") as fh:
+        json.dump(pmc, fh, indent=1)
+    traffic["source"] = f"profiles/{rn}_pmc.json (rocprofv3 --pmc, tools/pmc.sh)"
+    with open(os.path.join(dst, "pmc_traffic.json"), "w") as fh:
+        json.dump(traffic, fh, indent=1)
+    print("collected", rn)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
