@@ -45,7 +45,7 @@ def test_config4_five_mixed_fields_256_h3():
     obufs = orc.regular_exchange([rf], {0: opat}, 1)
     co = R.make_communication_object(ctx)
     co.exchange(bis).wait()
-    (pair, ob), = obufs.items()
+    ((_, pair), ob), = obufs.items()
     send = co.buffers(co.plan(bis), bases[0].device)[0][0]
     items = [(k, 0, opat[0][0], f[0].elem, f[0].data.dtype.alignment, 1, 0) for k, f in enumerate(rf)]
     pb = orc.plan_buffers(items, receive=False)[pair]
