@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--N", type=int, default=512)
     p.add_argument("--halo", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph")
+    p.add_argument("--unfused", action="store_true",
+                   help="N=1: time pack and unpack as two launches instead of the fused self exchange")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true")
@@ -128,23 +130,37 @@ def main():
         if rc:
             raise RuntimeError(L.ghx_last_error().decode())
 
-    def step():
+    def fused(s):
+        rc = L.ghx_exchange_self(plan.h, fptr, 1, sptr, ns, s)
+        if rc:
+            raise RuntimeError(L.ghx_last_error().decode())
+
+    # The product's exchange step: at N=1 every message is a self message and the communication
+    # object runs pack+unpack as ONE launch (ghx_exchange_self); otherwise pack, transport, unpack.
+    use_fused = co.fuse_self and co.all_self(plan) and not args.unfused
+
+    def step_unfused():
         s = torch.cuda.current_stream(dev).cuda_stream
         pack(s)
         unpack(s)
 
-    graph = None
-    if not args.no_graph:
+    def step_fused():
+        fused(torch.cuda.current_stream(dev).cuda_stream)
+
+    def make_run(step):
+        if args.no_graph:
+            return step
         side = torch.cuda.Stream(dev)
         side.wait_stream(stream)
         with torch.cuda.stream(side):
             step()  # warm the capture stream
         stream.wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
             step()
-    run = graph.replay if graph is not None else step
+        return g.replay
 
+    run = make_run(step_fused if use_fused else step_unfused)
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize(dev)
@@ -178,7 +194,9 @@ def main():
             "workload": f"{N}^3 fp64 structured 3D halo={Hw}, 26-neighbour periodic, "
                         f"device-resident pack+unpack, decomposition {list(parts)}",
             "N": N, "halo": Hw, "fields": 1, "decomposition": list(parts),
-            "launch": "hipGraph" if graph is not None else "eager",
+            "launch": ("eager" if args.no_graph else "hipGraph") + ", " +
+                      ("fused self-exchange: 1 launch per step (pack tile -> workgroup barrier "
+                       "-> unpack same bytes)" if use_fused else "pack launch + unpack launch"),
             "bytes_per_step_per_gpu": step_bytes,
             "parallelism": f"{world} rank(s), one domain per GPU",
         },
@@ -189,9 +207,14 @@ def main():
     # Differential method (removes the fixed cost of the events themselves): hipGraphs of M steps,
     # of M steps + one pack, and of M steps + one pack + one unpack, replayed in interleaved
     # rounds; pack = T1 - T0, unpack = T2 - T1 (each includes its dependent-launch boundary).
-    t_pack, t_unpack = kernel_durations(torch, dev, stream, pack, unpack)
-    launch_bytes = 2 * n_halo * 8
-    dom_name, dom_t = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+    t_pack, t_unpack = kernel_durations(torch, dev, stream, [pack, unpack])
+    if use_fused:
+        (t_fused,) = kernel_durations(torch, dev, stream, [fused])
+        launch_bytes, dom_name, dom_t, kname = step_bytes, "self", t_fused, "k_self (pack+unpack)"
+    else:
+        launch_bytes = 2 * n_halo * 8
+        dom_name, dom_t = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+        kname = f"k_copy<{dom_name}>"
     achieved = launch_bytes / dom_t / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -202,11 +225,20 @@ def main():
             traffic = ent.get("hbm_bytes_per_launch") if ent else None
         except Exception:
             traffic = None
-    out["roofline"] = {"bound": "hbm", "kernel": f"k_structured<{dom_name}>",
+    out["roofline"] = {"bound": "hbm", "kernel": kname,
                        "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                        "algorithmic_bytes_per_launch": launch_bytes,
+                       "launch_us": round(dom_t * 1e6, 2),
                        "pack_us": round(t_pack * 1e6, 2), "unpack_us": round(t_unpack * 1e6, 2)}
+    if use_fused:
+        # the same step as two launches (what N>1 runs per rank), for comparison
+        run_u = make_run(step_unfused)
+        for _ in range(5):
+            run_u()
+        Tu = timed(run_u, K)
+        out["unfused"] = {"value": round(world * step_bytes * K / Tu / 1e9, 2),
+                          "ms_per_step": round(Tu / K * 1e3, 5)}
 
     if not args.no_extras:
         # full exchange incl. transport (RCCL for N>1; self-message aliasing for N=1)
@@ -249,29 +281,29 @@ def main():
         dist.destroy_process_group()
 
 
-def kernel_durations(torch, dev, stream, pack, unpack, M=10, rounds=15):
+def kernel_durations(torch, dev, stream, fns, M=10, rounds=15):
+    """Live per-launch durations of the launches `fns` (one step = fns in order) by differencing
+    hipGraphs of M steps, M steps + fns[0], M steps + fns[0] + fns[1], ... replayed in interleaved
+    rounds (medians). Removes the events' own cost; each includes its dependent-launch boundary."""
     def capture(extra):
         g = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(dev)
         side.wait_stream(stream)
         with torch.cuda.stream(side):
-            s = side.cuda_stream
-            pack(s)
-            unpack(s)
+            for f in fns:
+                f(side.cuda_stream)
         stream.wait_stream(side)
         with torch.cuda.graph(g):
             s = torch.cuda.current_stream(dev).cuda_stream
             for _ in range(M):
-                pack(s)
-                unpack(s)
-            if extra >= 1:
-                pack(s)
-            if extra >= 2:
-                unpack(s)
+                for f in fns:
+                    f(s)
+            for f in fns[:extra]:
+                f(s)
         return g
 
-    graphs = [capture(e) for e in range(3)]
-    times = [[], [], []]
+    graphs = [capture(e) for e in range(len(fns) + 1)]
+    times = [[] for _ in graphs]
     for g in graphs:
         g.replay()
     torch.cuda.synchronize(dev)
@@ -284,7 +316,7 @@ def kernel_durations(torch, dev, stream, pack, unpack, M=10, rounds=15):
             e1.synchronize()
             times[i].append(e0.elapsed_time(e1) * 1e-3)
     med = [sorted(t)[len(t) // 2] for t in times]
-    return med[1] - med[0], med[2] - med[1]
+    return tuple(med[i + 1] - med[i] for i in range(len(fns)))
 
 
 def cpu_baseline(N, Hw, seconds):

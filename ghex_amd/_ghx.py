@@ -87,6 +87,8 @@ _SIGS = {
                                     P(c_u64)]),
     "ghx_exchange_pack": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
     "ghx_exchange_unpack": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_exchange_self_fusable": (c_i32, [c_vp, P(c_i32)]),
+    "ghx_exchange_self": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
 }
 EXPORTED = tuple(_SIGS)
 

@@ -103,11 +103,21 @@ class CommunicationHandle:
 class CommunicationObject:
     """communication_object<grid, domain_id> (make_communication_object, :1105-1112)."""
 
-    def __init__(self, context):
+    def __init__(self, context, fuse_self: bool = True):
         self.context = context
+        self.fuse_self = fuse_self
         self._plans = {}
         self._bufs = {}
         self._valid = False
+
+    def all_self(self, plan) -> bool:
+        """Every message is a self message and libghx can fuse pack+unpack (ghx_exchange_self)."""
+        if getattr(plan, "_all_self", None) is None:
+            me = self.context.rank()
+            f = ctypes.c_int32()
+            _ghx.call("ghx_exchange_self_fusable", plan.h, ctypes.byref(f))
+            plan._all_self = bool(f.value) and all(b["rank"] == me for b in plan.send + plan.recv)
+        return plan._all_self
 
     # -- planning -----------------------------------------------------------------------------
     def _key(self, bis):
@@ -185,6 +195,13 @@ class CommunicationObject:
         sptrs = _ghx.ptr_array([t.data_ptr() for t in send])
         rptrs = _ghx.ptr_array([t.data_ptr() for t in recv])
         self._valid = True
+        if self.fuse_self and self.all_self(plan):
+            # every message stays on this device: pack + unpack in one launch
+            _ghx.call("ghx_exchange_self", plan.h, fptrs, len(bis), sptrs, len(send),
+                      stream.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            return CommunicationHandle(self, stream, ev)
         _ghx.call("ghx_exchange_pack", plan.h, fptrs, len(bis), sptrs, len(send),
                   stream.cuda_stream)
         me = self.context.rank()

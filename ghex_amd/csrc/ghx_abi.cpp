@@ -123,6 +123,30 @@ struct exchange_plan
     std::unique_ptr<splan> spack, sunpack;
     std::unique_ptr<uplan> upack, uunpack;
     int32_t n_items = 0;
+    mutable int self_ok = -1;  // lazily checked: may pack and unpack be fused (all self)?
+
+    // Every recv buffer aliases the send buffer of the same pair, and pack segment k and unpack
+    // segment k cover the same buffer bytes with the same tiling.
+    bool self_fusable() const
+    {
+        if (self_ok >= 0) return self_ok == 1;
+        bool ok = !upack && !uunpack && spack && sunpack && send.size() == recv.size();
+        for (size_t i = 0; ok && i < send.size(); ++i)
+            ok = send[i].first_id == recv[i].first_id && send[i].second_id == recv[i].second_id &&
+                 send[i].size == recv[i].size;
+        if (ok) ok = spack->host_segs.size() == sunpack->host_segs.size() &&
+                     spack->n_tiles == sunpack->n_tiles;
+        for (size_t k = 0; ok && k < spack->host_segs.size(); ++k)
+        {
+            const auto& a = spack->host_segs[k];
+            const auto& b = sunpack->host_segs[k];
+            ok = a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
+                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes && a.partner < 0 &&
+                 b.partner < 0;
+        }
+        self_ok = ok ? 1 : 0;
+        return ok;
+    }
 };
 }  // namespace ghx
 
@@ -714,6 +738,46 @@ int ghx_exchange_unpack(const ghx_exchange* ex, void* const* field_ptrs, int32_t
         if (rc == GHX_OK && ex->uunpack)
             rc = ex->uunpack->execute(field_ptrs, n_fields, recv_buffers, n_recv, stream);
         return rc;
+    });
+}
+
+int ghx_exchange_self_fusable(const ghx_exchange* ex, int32_t* fusable)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        check_ptr(fusable, "fusable");
+        *fusable = ex->self_fusable() ? 1 : 0;
+        return GHX_OK;
+    });
+}
+
+int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                      void* const* buffers, int32_t n_buffers, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        if (!ex->self_fusable())
+            throw invalid("exchange is not an all-self exchange with matching segments");
+        const splan& p = *ex->spack;
+        if (n_fields <= p.max_field_slot || n_buffers <= p.max_buf_slot)
+            throw invalid("pointer arrays do not cover the plan's slots");
+        if (!p.dev.segs || !ex->sunpack->dev.segs) throw hip_error("plan has no device tables");
+        kargs a{};
+        a.segs = p.dev.segs;
+        a.segs2 = ex->sunpack->dev.segs;
+        a.tile_seg = p.dev.tiles;
+        a.n_tiles = p.n_tiles;
+        for (int i = 0; i <= p.max_field_slot; ++i)
+        {
+            if (!field_ptrs[i]) throw invalid("null field pointer");
+            a.field_ptr[i] = reinterpret_cast<uint64_t>(field_ptrs[i]);
+        }
+        for (int i = 0; i <= p.max_buf_slot; ++i)
+        {
+            if (!buffers[i]) throw invalid("null buffer pointer");
+            a.buf_ptr[i] = reinterpret_cast<uint64_t>(buffers[i]);
+        }
+        return launch_self(a, stream, grid_for_tiles(p.n_tiles));
     });
 }
 

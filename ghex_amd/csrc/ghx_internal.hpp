@@ -118,6 +118,7 @@ static_assert(sizeof(seg_u) == 96, "seg_u layout");
 struct kargs
 {
     const void* segs;
+    const void* segs2;         // fused self exchange: the unpack segments (1:1 with segs)
     const uint32_t* tile_seg;  // per tile: {segment index, tile index within the segment}
     uint32_t n_tiles;
     uint32_t pad0;
@@ -132,6 +133,7 @@ const char* get_error();
 // kernel launchers (ghx_kernels.hip)
 int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid);
 int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid);
+int launch_self(const kargs& a, void* stream, uint32_t grid);
 uint32_t grid_for_tiles(uint32_t n_tiles);
 
 }  // namespace ghx

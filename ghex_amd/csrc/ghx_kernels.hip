@@ -309,6 +309,51 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
     }
 }
 
+template<bool PACK, int U, int NT>
+__device__ __forceinline__ void copy_any(const seg_s& s, char* field, char* buf, uint32_t start,
+                                         uint32_t end, int w)
+{
+    switch (w)
+    {
+        case 4: copy_tile<PACK, 16, U, NT>(s, field, buf, start, end); break;
+        case 3: copy_tile<PACK, 8, U, NT>(s, field, buf, start, end); break;
+        case 2: copy_tile<PACK, 4, U, NT>(s, field, buf, start, end); break;
+        case 1: copy_tile<PACK, 2, U, NT>(s, field, buf, start, end); break;
+        default: copy_tile<PACK, 1, U, NT>(s, field, buf, start, end); break;
+    }
+}
+
+// Fused self exchange: every message is a self message, so pack segment k and unpack segment k
+// cover the same buffer bytes. A workgroup packs its tile (field interior -> buffer), waits at a
+// workgroup barrier (its own stores are visible to its own waves), then unpacks the same bytes
+// (buffer -> field halo). All bytes of pack and unpack move; the hand-off never leaves the CU.
+template<int U, int NT>
+__global__ __launch_bounds__(kBlock) void k_self(kargs a)
+{
+    const seg_s* __restrict__ ps = static_cast<const seg_s*>(a.segs);
+    const seg_s* __restrict__ us = static_cast<const seg_s*>(a.segs2);
+    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
+    {
+        const uint32_t si = a.tile_seg[2 * t];
+        const uint32_t ti = a.tile_seg[2 * t + 1];
+        const seg_s s = ps[si];
+        const seg_s q = us[si];
+        const uint32_t start = ti * s.tile_bytes;
+        const uint32_t end = min(start + s.tile_bytes, s.bytes);
+        char* field_p = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
+        char* field_u = reinterpret_cast<char*>(a.field_ptr[q.field_slot]);
+        char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
+        int wp = min(int(s.wlog2), ptr_wlog2(reinterpret_cast<uint64_t>(field_p)));
+        wp = min(wp, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+        int wu = min(int(q.wlog2), ptr_wlog2(reinterpret_cast<uint64_t>(field_u)));
+        wu = min(wu, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+        copy_any<true, U, NT>(s, field_p, buf, start, end, wp);
+        __syncthreads();  // workgroup release/acquire: the tile's buffer bytes are complete
+        copy_any<false, U, NT>(q, field_u, buf, start, end, wu);
+        __syncthreads();  // keep tiles of a grid-stride loop ordered for the next iteration
+    }
+}
+
 template<typename Seg, bool PACK, int U>
 void launch_nt(const kargs& a, hipStream_t s, uint32_t grid)
 {
@@ -346,6 +391,22 @@ int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid
     if (e != hipSuccess)
     {
         set_error(std::string("structured kernel launch failed: ") + hipGetErrorString(e));
+        return GHX_ERR_HIP;
+    }
+    return GHX_OK;
+}
+
+int launch_self(const kargs& a, void* stream, uint32_t grid)
+{
+    if (a.n_tiles == 0) return GHX_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (g_tune.unroll == 8) hipLaunchKernelGGL((k_self<8, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (g_tune.unroll == 2) hipLaunchKernelGGL((k_self<2, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_self<4, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+    {
+        set_error(std::string("self-exchange kernel launch failed: ") + hipGetErrorString(e));
         return GHX_ERR_HIP;
     }
     return GHX_OK;

@@ -270,6 +270,17 @@ int ghx_exchange_pack(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
 int ghx_exchange_unpack(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
                         void* const* recv_buffers, int32_t n_recv, ghx_stream stream);
 
+/* Self messages (a periodic wrap onto the same rank, or two domains of one rank) never leave
+ * the device in the reference's stream-aware flow either (communication_object.hpp:703-767:
+ * pack -> send to self -> unpack). When EVERY message of an exchange is a self message
+ * (*fusable = 1), ghx_exchange_self performs pack and unpack in ONE launch: each workgroup packs
+ * a tile of the send buffer and then unpacks the same bytes into the halos (workgroup barrier in
+ * between). The buffers are the send buffers (they double as recv buffers); every byte of both
+ * pack and unpack is moved, and the send buffers hold the packed message afterwards. */
+int ghx_exchange_self_fusable(const ghx_exchange* ex, int32_t* fusable);
+int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                      void* const* buffers, int32_t n_buffers, ghx_stream stream);
+
 #ifdef __cplusplus
 }
 #endif
