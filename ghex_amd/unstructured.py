@@ -10,8 +10,8 @@ from .communication_object import CommunicationObject
 from .pattern import PatternContainer
 
 
-def make_communication_object(context) -> CommunicationObject:
-    return CommunicationObject(context)
+def make_communication_object(context, **options) -> CommunicationObject:
+    return CommunicationObject(context, **options)
 
 
 class DomainDescriptor:
