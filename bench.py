@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--N", type=int, default=512)
     p.add_argument("--halo", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph")
+    p.add_argument("--steps-per-graph", type=int, default=10,
+                   help="steps captured per hipGraph (the K timed steps replay K/G graphs)")
     p.add_argument("--unfused", action="store_true",
                    help="N=1: time pack and unpack as two launches instead of the fused self exchange")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -148,21 +150,40 @@ def main():
         fused(torch.cuda.current_stream(dev).cuda_stream)
 
     def make_run(step):
+        """run(k): exactly k steps, replayed from hipGraphs of G = --steps-per-graph steps
+        (+ one graph for the remainder), so the graph-launch cost is paid once per G steps."""
         if args.no_graph:
-            return step
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(stream)
-        with torch.cuda.stream(side):
-            step()  # warm the capture stream
-        stream.wait_stream(side)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            step()
-        return g.replay
+            def run_eager(k):
+                for _ in range(k):
+                    step()
+            return run_eager
+        graphs = {}
+
+        def graph_of(n):
+            if n not in graphs:
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(stream)
+                with torch.cuda.stream(side):
+                    step()  # warm the capture stream
+                stream.wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(n):
+                        step()
+                graphs[n] = g
+            return graphs[n]
+
+        G = max(1, args.steps_per_graph)
+
+        def run(k):
+            for _ in range(k // G):
+                graph_of(G).replay()
+            if k % G:
+                graph_of(k % G).replay()
+        return run
 
     run = make_run(step_fused if use_fused else step_unfused)
-    for _ in range(args.warmup):
-        run()
+    run(args.warmup)
     torch.cuda.synchronize(dev)
 
     def timed(fn, k):
@@ -183,7 +204,9 @@ def main():
         return dt
 
     K = args.steps
-    T = timed(run, K)
+    run(K % max(1, args.steps_per_graph) or 1)  # instantiate the remainder graph untimed
+    torch.cuda.synchronize(dev)
+    T = timed(lambda: run(K), 1)
     value = world * step_bytes * K / T / 1e9
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
@@ -194,7 +217,8 @@ def main():
             "workload": f"{N}^3 fp64 structured 3D halo={Hw}, 26-neighbour periodic, "
                         f"device-resident pack+unpack, decomposition {list(parts)}",
             "N": N, "halo": Hw, "fields": 1, "decomposition": list(parts),
-            "launch": ("eager" if args.no_graph else "hipGraph") + ", " +
+            "launch": ("eager" if args.no_graph else
+                       f"hipGraph of {args.steps_per_graph} steps") + ", " +
                       ("fused self-exchange: 1 launch per step (pack tile -> workgroup barrier "
                        "-> unpack same bytes)" if use_fused else "pack launch + unpack launch"),
             "bytes_per_step_per_gpu": step_bytes,
@@ -234,9 +258,8 @@ def main():
     if use_fused:
         # the same step as two launches (what N>1 runs per rank), for comparison
         run_u = make_run(step_unfused)
-        for _ in range(5):
-            run_u()
-        Tu = timed(run_u, K)
+        run_u(max(5, K % max(1, args.steps_per_graph)))
+        Tu = timed(lambda: run_u(K), 1)
         out["unfused"] = {"value": round(world * step_bytes * K / Tu / 1e9, 2),
                           "ms_per_step": round(Tu / K * 1e3, 5)}
 

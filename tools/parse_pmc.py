@@ -15,13 +15,16 @@ def main(d):
     for p in sorted(glob.glob(f"{d}/p*/pmc_counter_collection.csv")):
         for row in csv.DictReader(open(p)):
             k = row["Kernel_Name"]
-            if "k_copy" not in k:
+            if "k_self" in k:
+                kind = "self"
+            elif "k_copy" in k:
+                kind = "pack" if "k_copy<true" in k else "unpack"
+            else:
                 continue
-            kind = "pack" if "k_copy<true" in k else "unpack"
             acc[(kind, row["Counter_Name"])].append(float(row["Counter_Value"]))
     med = {k: sorted(v)[len(v) // 2] for k, v in acc.items()}
     out = {}
-    for kind in ("pack", "unpack"):
+    for kind in sorted({k for k, _ in med}):
         g = lambda c: med.get((kind, c))
         r = {c: g(c) for c in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum",
                                "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum",
