@@ -295,6 +295,16 @@ def main():
             # restore valid halos after the staged copies
             co.exchange(bis).wait()
 
+    if world == 1 and not args.no_extras:
+        # the other BASELINE configs, per GPU (their 8-GPU forms are weak-scaled copies)
+        del base, logical, fd, bis, send, recv
+        co = None
+        torch.cuda.empty_cache()
+        out["extra_configs"] = {
+            "config4_5fields_256^3_h3_f64f32": bench_config4(torch, dev, ghex_amd, R),
+            "config5_unstructured_10M_5pct_levels1": bench_config5(torch, dev, _ghx, 1),
+            "config5_unstructured_10M_5pct_levels8": bench_config5(torch, dev, _ghx, 8),
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, Hw, args.cpu_seconds)
     if rank == 0:
@@ -340,6 +350,119 @@ def kernel_durations(torch, dev, stream, fns, M=10, rounds=15):
             times[i].append(e0.elapsed_time(e1) * 1e-3)
     med = [sorted(t)[len(t) // 2] for t in times]
     return tuple(med[i + 1] - med[i] for i in range(len(fns)))
+
+
+def _time_graph(torch, dev, fn, k=50, per=10):
+    stream = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(stream)
+    with torch.cuda.stream(side):
+        fn(side.cuda_stream)
+    stream.wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per):
+            fn(torch.cuda.current_stream(dev).cuda_stream)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(k // per):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / (k // per * per)
+
+
+def bench_config4(torch, dev, ghex_amd, R):
+    """BASELINE config 4 on one GPU: 5 fields 256^3 [f64,f32,f64,f32,f64], H=3, one exchange of
+    all five (one periodic domain: all self messages -> the fused launch), verified."""
+    from ghex_amd import _ghx
+    N, H = 256, 3
+    E = N + 2 * H
+    types = [torch.float64, torch.float32, torch.float64, torch.float32, torch.float64]
+    ctx = ghex_amd.make_context()
+    dd = R.DomainDescriptor(0, (0, 0, 0), (N - 1,) * 3)
+    pc = R.make_pattern(ctx, R.HaloGenerator((0, 0, 0), (N - 1,) * 3, (H,) * 6, (True,) * 3), [dd])
+    fields, bis = [], []
+    ar = torch.arange(N, device=dev, dtype=torch.float64)
+    val = (ar.view(1, 1, N) + N * (ar.view(1, N, 1) + N * ar.view(N, 1, 1)))
+    for k, T in enumerate(types):
+        f = torch.full((E, E, E), -1, dtype=T, device=dev)
+        f[H:H + N, H:H + N, H:H + N] = ((val + k) % (1 << 23)).to(T)
+        fields.append(f)
+        bis.append(pc(R.make_field_descriptor(dd, f.permute(2, 1, 0), (H,) * 3, (E,) * 3)))
+    co = R.make_communication_object(ctx)
+    co.exchange(bis).wait()
+    idx = (torch.arange(E, device=dev) - H) % N
+    wv = (idx.view(1, 1, E) + N * (idx.view(1, E, 1) + N * idx.view(E, 1, 1))).to(torch.float64)
+    ok = all(bool((f == ((wv + k) % (1 << 23)).to(f.dtype)).all()) for k, f in enumerate(fields))
+    plan = co.plan(bis)
+    send, recv = co.buffers(plan, dev)
+    fptr = _ghx.ptr_array([f.data_ptr() for f in fields])
+    sptr = _ghx.ptr_array([t.data_ptr() for t in send])
+    L = _ghx.lib()
+    fusedp = co.all_self(plan)
+
+    def step(s):
+        if fusedp:
+            L.ghx_exchange_self(plan.h, fptr, 5, sptr, len(send), s)
+        else:
+            L.ghx_exchange_pack(plan.h, fptr, 5, sptr, len(send), s)
+            L.ghx_exchange_unpack(plan.h, fptr, 5, sptr, len(send), s)
+    t = _time_graph(torch, dev, step)
+    n = E ** 3 - N ** 3
+    nbytes = 4 * n * (3 * 8 + 2 * 4)
+    return {"GBps": round(nbytes / t / 1e9, 1), "us_per_exchange": round(t * 1e6, 2),
+            "bytes_per_exchange": nbytes, "verified": ok, "fused_self": fusedp}
+
+
+def bench_config5(torch, dev, _ghx, levels):
+    """BASELINE config 5 shape on one GPU: 10M cells (levels=1) / 2M cells (levels=8),
+    5 % halo, 7 peers, random lids (seed 20260715), levels_first fp64: fused gather of all
+    send lists + fused scatter of all recv lists (unstructured plans)."""
+    import ctypes
+    import numpy as np
+    rng = np.random.default_rng(20260715)
+    n = 10_000_000 if levels == 1 else 2_000_000
+    nh = n // 20
+    send = rng.choice(n, size=nh, replace=False)
+    recv = rng.permutation(n)[:nh]
+    cuts = np.sort(rng.choice(np.arange(1, nh), size=6, replace=False))
+    sl, rl = np.split(send, cuts), np.split(recv, cuts)
+    vals = torch.randn(n * levels, dtype=torch.float64, device=dev)
+
+    def plan(lists, direction):
+        ents, keep = [], []
+        for k, l in enumerate(lists):
+            e = _ghx.UPackEntry()
+            e.data.elem_size, e.data.levels, e.data.levels_first = 8, levels, 1
+            e.data.index_stride, e.data.level_stride = levels, 1
+            e.field_slot, e.buffer_slot, e.buffer_offset = 0, k, 0
+            arr = np.ascontiguousarray(l, dtype=np.int64)
+            keep.append(arr)
+            e.lids = arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+            e.n_lids = len(arr)
+            ents.append(e)
+        h = ctypes.c_void_p()
+        _ghx.call("ghx_uplan_create", (_ghx.UPackEntry * len(ents))(*ents), len(ents), direction,
+                  ctypes.byref(h))
+        return h
+
+    hp, hu = plan(sl, 0), plan(rl, 1)
+    bufs = [torch.empty(len(l) * levels * 8, dtype=torch.uint8, device=dev) for l in sl]
+    fp = _ghx.ptr_array([vals.data_ptr()])
+    bp = _ghx.ptr_array([b.data_ptr() for b in bufs])
+    L = _ghx.lib()
+
+    def step(s):
+        L.ghx_uplan_execute(hp, fp, 1, bp, len(bufs), s)
+        L.ghx_uplan_execute(hu, fp, 1, bp, len(bufs), s)
+    t = _time_graph(torch, dev, step)
+    L.ghx_uplan_destroy(hp)
+    L.ghx_uplan_destroy(hu)
+    nbytes = 4 * nh * levels * 8
+    return {"GBps": round(nbytes / t / 1e9, 1), "us_per_exchange": round(t * 1e6, 2),
+            "bytes_per_exchange": nbytes, "cells": n, "halo_cells": nh, "peers": 7,
+            "index_bytes_per_exchange": 2 * nh * 4}
 
 
 def cpu_baseline(N, Hw, seconds):
