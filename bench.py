@@ -6,10 +6,14 @@ Workload (BASELINE configs[1], weak-scaled for N>1 as configs[2]): per GPU one 5
 iteration spaces are a self message); N=2/4/8: (2,1,1)/(2,2,1)/(2,2,2) decomposition of the
 periodic global grid, one rank per GPU.
 
-A step = one fused pack launch (every iteration space of every send buffer) + one fused unpack
-launch (every recv buffer), with fields and buffers resident in HBM. Algorithmic bytes per step
-per GPU = 4 * n * 8 (pack read + write, unpack read + write), n = (N+2H)^3 - N^3 halo cells.
-value = sum over ranks of bytes*K / max over ranks of the K-step wall time.
+A step = the product's exchange step minus transport, fields and buffers resident in HBM: for
+N>1 one fused pack launch (every iteration space of every send buffer) + one fused unpack launch
+(every recv buffer); at N=1 every message is a self message and the communication object runs
+pack+unpack as ONE launch (ghx_exchange_self: each workgroup packs a tile of the buffer, then
+unpacks the same bytes; `--unfused` times the two-launch form, also reported as "unfused").
+Algorithmic bytes per step per GPU = 4 * n * 8 (pack read + write, unpack read + write),
+n = (N+2H)^3 - N^3 halo cells. value = sum over ranks of bytes*K / max over ranks of the K-step
+wall time; the K steps replay hipGraphs of --steps-per-graph steps.
 
 Before timing, one full exchange (pack -> RCCL send/recv over xGMI for N>1 -> unpack) is run and
 every cell of every rank's (N+2H)^3 box is verified on the GPU against the wrapped global index.
@@ -47,6 +51,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     p.add_argument("--tune", default="", help="developer: ghx_tune key=value,... before planning")
+    p.add_argument("--force-dist", action="store_true",
+                   help="initialise the nccl process group even at world size 1 (path test)")
     return p.parse_args()
 
 
@@ -63,7 +69,8 @@ def main():
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or args.force_dist
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     import ghex_amd
@@ -105,7 +112,7 @@ def main():
     bad = int((base != expect).sum().item())
     del expect
     verified = bad == 0
-    if world > 1:
+    if distributed:
         t = torch.tensor([bad], device=dev)
         dist.all_reduce(t)
         verified = int(t.item()) == 0
@@ -187,17 +194,17 @@ def main():
     torch.cuda.synchronize(dev)
 
     def timed(fn, k):
-        if world > 1:
+        if distributed:
             dist.barrier(device_ids=[local])
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(k):
             fn()
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if distributed:
             dist.barrier(device_ids=[local])
         dt = time.perf_counter() - t0
-        if world > 1:
+        if distributed:
             tt = torch.tensor([dt], device=dev, dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             dt = float(tt.item())
@@ -309,7 +316,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(N, Hw, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier(device_ids=[local])
         dist.destroy_process_group()
 
