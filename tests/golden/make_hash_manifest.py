@@ -1,0 +1,85 @@
+"""Generate tests/golden/hash_manifest.json: FNV-1a-64 checksums of every packed message and of
+every field after unpack, computed by the oracle (oracle/oracle.py regular_exchange, the
+restatement of communication_object::pack/unpack + serialization<cpu>, pinned to the
+reference's halo generator by tests/test_oracle.py). SURVEY.md §8(c) fixture plan, item 2.
+
+Run in the build container:  python tests/golden/make_hash_manifest.py [--no-full]
+
+Cases (all periodic, cube_domains geometry, owned cell = global linear index, halos -1):
+  small: N in {8, 13} x H in {1, 2, 3} x the 6 layout maps x decompositions 1, (2,1,1), (2,2,2)
+  asym : N=8, field offset 2, halos {0,0,1,0,1,2} (test_regular_domain.cpp pattern 1), (2,1,1)
+  full : 512^3 fp64 H in {1, 2, 3} on one rank (BASELINE config 2), and 2x2x2 at N=64 H=2
+The GPU tests recompute the same checksums from the HIP path (tests/test_gpu_manifest.py);
+tests/test_oracle.py re-derives the small cases from the oracle (regression pin)."""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as orc  # noqa: E402
+from tests import helpers as H  # noqa: E402
+
+LAYOUTS = [(2, 1, 0), (0, 1, 2), (1, 2, 0), (2, 0, 1), (1, 0, 2), (0, 2, 1)]
+PARTS = [(1, 1, 1), (2, 1, 1), (2, 2, 2)]
+ASYM = (0, 0, 1, 0, 1, 2)
+
+
+def case_name(N, Hw, layout, parts, halos=None):
+    s = f"N{N}_H{Hw}_L{''.join(map(str, layout))}_P{''.join(map(str, parts))}"
+    return s if halos is None else s + "_A" + "".join(map(str, halos))
+
+
+def run_case(N, Hw, layout, parts, halos=None):
+    """Oracle exchange of one linear-index field per rank. Returns the manifest entry:
+    {"messages": {"<rank>:<recv dom>,<send dom>": [size, fnv]}, "fields": [fnv per rank]}."""
+    halos = tuple(halos) if halos is not None else (Hw,) * 6
+    ranks, gf, gl = H.cube_domains(N, parts)
+    nr = len(ranks)
+    opat = orc.regular_make_pattern(ranks, gf, gl, halos, (1, 1, 1))
+    arrs, rf = [], []
+    for r in range(nr):
+        a, spec = H.linear_index_field(ranks[r][0], N, Hw, gl, layout=layout)
+        arrs.append(a)
+        rf.append([(spec, ranks[r][0].id, 0, 0)])
+    bufs = orc.regular_exchange(rf, {0: opat}, nr)
+    msgs = {f"{r}:{pair[0]},{pair[1]}": [int(b.size), f"{orc.fnv1a64(b):016x}"]
+            for (r, pair), b in sorted(bufs.items())}
+    return {"messages": msgs, "fields": [f"{orc.fnv1a64(a):016x}" for a in arrs]}
+
+
+def small_cases():
+    for N in (8, 13):
+        for Hw in (1, 2, 3):
+            for layout in LAYOUTS:
+                for parts in PARTS:
+                    yield (N, Hw, layout, parts, None)
+    yield (8, 2, (2, 1, 0), (2, 1, 1), ASYM)
+
+
+def full_cases():
+    for Hw in (1, 2, 3):
+        yield (512, Hw, (2, 1, 0), (1, 1, 1), None)
+    yield (64, 2, (2, 1, 0), (2, 2, 2), None)
+
+
+def main(full=True):
+    out = {"generator": "tests/golden/make_hash_manifest.py (oracle regular_exchange)",
+           "hash": "FNV-1a 64 over the bytes (offset basis 0xcbf29ce484222325)",
+           "small": {}, "full": {}}
+    for c in small_cases():
+        out["small"][case_name(*c)] = run_case(*c)
+    if full:
+        for c in full_cases():
+            out["full"][case_name(*c)] = run_case(*c)
+            print("full case", case_name(*c), flush=True)
+    with open(os.path.join(HERE, "hash_manifest.json"), "w") as fh:
+        json.dump(out, fh, indent=0, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(full="--no-full" not in sys.argv)

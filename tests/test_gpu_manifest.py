@@ -1,0 +1,92 @@
+"""GPU parity against the committed checksum manifest (tests/golden/hash_manifest.json, made by
+tests/golden/make_hash_manifest.py from the oracle): every packed message and every field after
+unpack, FNV-1a 64, for 109 small cases (2 cube sizes x 3 halos x 6 layout maps x 3
+decompositions + asymmetric halos) and the full-size cases (512^3 fp64 H=1/2/3 on one rank —
+BASELINE config 2 — and 2x2x2 ranks of 64^3). Multi-rank cases are emulated in one process
+(tests/gpu_util.emulated_exchange); single-rank cases run the communication object's own
+exchange(), i.e. the fused self-exchange kernel the bench measures."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+MANIFEST = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                       "hash_manifest.json")))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ghex_amd
+    ghex_amd.native_library()
+
+
+def _parse(name):
+    parts = dict((p[0], p[1:]) for p in name.split("_"))
+    halos = tuple(int(c) for c in parts["A"]) if "A" in parts else None
+    return (int(parts["N"]), int(parts["H"]), tuple(int(c) for c in parts["L"]),
+            tuple(int(c) for c in parts["P"]), halos)
+
+
+def gpu_case(N, Hw, layout, parts, halos=None):
+    import torch
+    from ghex_amd.structured import regular as R
+    from tests.gpu_util import FakeContext, device_field, emulated_exchange
+    halos = tuple(halos) if halos is not None else (Hw,) * 6
+    ranks, gf, gl = H.cube_domains(N, parts)
+    nr = len(ranks)
+    table = {r: [(d.id, d.first, d.last) for d in ranks[r]] for r in range(nr)}
+    E = N + 2 * Hw
+    cos, bis, bases = [], [], []
+    for r in range(nr):
+        ctx = FakeContext(r, nr, table)
+        dd = R.DomainDescriptor(ranks[r][0].id, ranks[r][0].first, ranks[r][0].last)
+        pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, halos, (1, 1, 1)), [dd])
+        a, _ = H.linear_index_field(ranks[r][0], N, Hw, gl, layout=layout)
+        base, logical = device_field(a, layout)
+        del a
+        fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (E,) * 3)
+        cos.append(R.make_communication_object(ctx))
+        bis.append([pc(fd)])
+        bases.append(base)
+    if nr == 1:
+        cos[0].exchange(bis[0]).wait()
+        plan = cos[0].plan(bis[0])
+        plans, bufs = [plan], [cos[0].buffers(plan, bases[0].device)]
+    else:
+        plans, bufs = emulated_exchange(cos, bis)
+    torch.cuda.synchronize()
+    msgs = {}
+    for r in range(nr):
+        for i, x in enumerate(plans[r].send):
+            b = bufs[r][0][i][:x["size"]].cpu().numpy()
+            msgs[f"{r}:{x['pair'][0]},{x['pair'][1]}"] = [int(x["size"]),
+                                                          f"{orc.fnv1a64(b):016x}"]
+    fields = [f"{orc.fnv1a64(b.cpu().numpy()):016x}" for b in bases]
+    return {"messages": msgs, "fields": fields}
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST["small"]))
+def test_small_case_matches_manifest(name):
+    got = gpu_case(*_parse(name))
+    exp = MANIFEST["small"][name]
+    assert got["messages"] == exp["messages"]
+    assert got["fields"] == exp["fields"]
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST["full"]))
+def test_full_case_matches_manifest(name):
+    import torch
+    got = gpu_case(*_parse(name))
+    exp = MANIFEST["full"][name]
+    assert got["messages"] == exp["messages"]
+    assert got["fields"] == exp["fields"]
+    torch.cuda.empty_cache()

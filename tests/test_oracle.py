@@ -208,3 +208,38 @@ def test_elementwise_equals_batch_for_unit_stride():
         assert orc.structured_pack(spec, b1, lst) == n
         orc.structured_pack(spec, b2, lst, elementwise=True)
         np.testing.assert_array_equal(b1, b2)
+
+
+def _manifest():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                       "hash_manifest.json")))
+
+
+def test_hash_manifest_small_cases_reproduce():
+    """The committed checksum manifest (the GPU tests' expected values) is what the oracle
+    produces today, for every small case (tests/golden/make_hash_manifest.py)."""
+    from tests.golden.make_hash_manifest import case_name, run_case, small_cases
+    m = _manifest()["small"]
+    cases = list(small_cases())
+    assert len(cases) == len(m) == 109
+    for c in cases:
+        assert run_case(*c) == m[case_name(*c)], case_name(*c)
+
+
+def test_hash_manifest_full_sizes_and_message_counts():
+    """Full-size entries: message sizes equal SURVEY §8(d)'s algorithmic bytes per direction
+    (n(512,H) * 8 B on one rank; 2x2x2: 7 peer messages per rank, 3 faces of 2*N^2*H, 3 edges
+    of 4*N*H^2, 1 corner of 8*H^3 elements)."""
+    m = _manifest()["full"]
+    n = {1: 1579016, 2: 3170368, 3: 4774104}
+    for Hw, cells in n.items():
+        e = m[f"N512_H{Hw}_L210_P111"]
+        assert list(e["messages"].values())[0][0] == cells * 8
+    e = m["N64_H2_L210_P222"]
+    for r in range(8):
+        sizes = sorted(v[0] for k, v in e["messages"].items() if k.startswith(f"{r}:"))
+        N, Hw = 64, 2
+        assert sizes == sorted([8 * 8 * Hw ** 3] + [8 * 4 * N * Hw * Hw] * 3
+                               + [8 * 2 * N * N * Hw] * 3)

@@ -22,13 +22,15 @@ def main(rn):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{rn}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
-    shutil.copy(os.path.join(src, "bench", "kt_kernel_stats.csv"),
-                os.path.join(dst, f"{rn}_bench_kernel_stats.csv"))
+    p = os.path.join(src, "bench", "kt_kernel_stats.csv")
+    if os.path.exists(p):
+        shutil.copy(p, os.path.join(dst, f"{rn}_bench_kernel_stats.csv"))
     for h in (1, 3):
         p = os.path.join(src, f"h{h}", "kt_kernel_stats.csv")
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, f"{rn}_h{h}_kernel_stats.csv"))
-    line = [l for l in open(os.path.join(src, "bench.log")) if l.startswith("{")]
+    blog = os.path.join(src, "bench.log")
+    line = [l for l in open(blog) if l.startswith("{")] if os.path.exists(blog) else []
     if line:
         with open(os.path.join(dst, f"{rn}_bench.json"), "w") as fh:
             fh.write(line[-1])
@@ -37,6 +39,11 @@ def main(rn):
         d = os.path.join(src, f"pmc_h{h}")
         if os.path.isdir(d):
             r = parse_pmc(d)
+            ds = os.path.join(src, f"pmc_h{h}_self")
+            if os.path.isdir(ds):
+                rs = parse_pmc(ds)
+                if "self" in rs:
+                    r["self"] = rs["self"]
             pmc[f"N512_H{h}"] = r
             traffic[f"N512_H{h}"] = {k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"]}
                                      for k, v in r.items()}
