@@ -302,6 +302,23 @@ def main():
             # restore valid halos after the staged copies
             co.exchange(bis).wait()
 
+    if not args.no_extras:
+        # measured device-to-device copy rate: 1 GiB -> 1 GiB, read+write bytes
+        a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        b = torch.empty_like(a)
+        for _ in range(3):
+            b.copy_(a)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        out["roofline"]["measured_d2d_copy_GBps"] = round(2 * a.numel() * 10 /
+                                                          (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+        del a, b
+        torch.cuda.empty_cache()
+
     if world == 1 and not args.no_extras:
         # the other BASELINE configs, per GPU (their 8-GPU forms are weak-scaled copies)
         del base, logical, fd, bis, send, recv
