@@ -303,6 +303,19 @@ def main():
             co.exchange(bis).wait()
 
     if not args.no_extras:
+        # the dominant launch with cold caches: an application's stencil sweeps the whole field
+        # between exchanges, so its halo rows are not left in the 256 MiB Infinity Cache as
+        # they are when the bench replays exchanges back to back. A 1 GiB read-modify-write
+        # before every launch evicts them; the flush itself is differenced away.
+        fl = torch.zeros(1 << 27, dtype=torch.float64, device=dev)
+        dom_fn = fused if use_fused else (pack if dom_name == "pack" else unpack)
+        t_cold = cold_duration(torch, dev, stream, dom_fn, lambda s: fl.add_(1.0))
+        out["roofline"]["cold_launch_us"] = round(t_cold * 1e6, 2)
+        out["roofline"]["cold_achieved"] = round(launch_bytes / t_cold / 1e9, 1)
+        del fl
+        torch.cuda.empty_cache()
+
+    if not args.no_extras:
         # measured device-to-device copy rate: 1 GiB -> 1 GiB, read+write bytes
         a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
         b = torch.empty_like(a)
@@ -374,6 +387,39 @@ def kernel_durations(torch, dev, stream, fns, M=10, rounds=15):
             times[i].append(e0.elapsed_time(e1) * 1e-3)
     med = [sorted(t)[len(t) // 2] for t in times]
     return tuple(med[i + 1] - med[i] for i in range(len(fns)))
+
+
+def cold_duration(torch, dev, stream, fn, flush, M=10, rounds=7):
+    """Per-launch duration of fn right after a cache-flushing kernel: median over rounds of
+    [graph of M x (flush, fn)] - [graph of M x flush], divided by M."""
+    def capture(with_fn):
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            flush(side.cuda_stream)
+            fn(side.cuda_stream)
+        stream.wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            s = torch.cuda.current_stream(dev).cuda_stream
+            for _ in range(M):
+                flush(s)
+                if with_fn:
+                    fn(s)
+        return g
+
+    g0, g1 = capture(False), capture(True)
+    t = [[], []]
+    for _ in range(rounds):
+        for i, g in enumerate((g0, g1)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            g.replay()
+            e1.record(stream)
+            e1.synchronize()
+            t[i].append(e0.elapsed_time(e1) * 1e-3)
+    med = [sorted(x)[len(x) // 2] for x in t]
+    return (med[1] - med[0]) / M
 
 
 def _time_graph(torch, dev, fn, k=50, per=10):

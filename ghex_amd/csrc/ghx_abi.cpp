@@ -289,7 +289,9 @@ int ghx_tune(const char* key, int32_t value)
     return guarded([&] {
         check_ptr(key, "key");
         const std::string k(key);
-        if (k == "unroll")
+        if (k == "reset")
+            g_tune = tuning{};
+        else if (k == "unroll")
         {
             if (value != 2 && value != 4 && value != 8) throw invalid("unroll must be 2, 4 or 8");
             g_tune.unroll = value;
@@ -308,6 +310,11 @@ int ghx_tune(const char* key, int32_t value)
         {
             if (value < 0 || value > 1) throw invalid("pair must be 0 or 1");
             g_tune.pair = value;
+        }
+        else if (k == "short_pol")
+        {
+            if (value < 0 || value > 3) throw invalid("short_pol must be in 0..3");
+            g_tune.short_pol = value;
         }
         else if (k == "small_row_bytes")
         {

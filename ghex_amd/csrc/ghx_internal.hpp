@@ -39,6 +39,9 @@ struct tuning
                                        // y+1 share a cache line): one lane moves both. Off by
                                        // default: with short-row-first dispatch the L2 already
                                        // merges the shared-line misses (same TCC_EA0_RDREQ)
+    int short_pol = 0;                 // field-side cache policy of short-row segments:
+                                       // bit 0 non-temporal loads (pack), bit 1 sc1 stores
+                                       // (unpack)
 };
 extern tuning g_tune;
 
@@ -80,7 +83,8 @@ struct alignas(16) seg_s
     uint16_t buf_slot;
     uint8_t wlog2;        // log2 of the widest vector (<= 16 B) that divides L, offsets, strides
     uint8_t n_outer;
-    uint8_t pad1[2];
+    uint8_t fpol;         // field-side cache policy: bit 0 nt loads, bit 1 sc1 stores
+    uint8_t pad1;
     uint32_t tile_bytes;  // this segment's tile size (a multiple of the row length or 16 KiB)
     int32_t partner;      // paired segment (row r here travels with its row r-1), or -1
     uint8_t pad[4];
@@ -108,7 +112,7 @@ struct alignas(16) seg_u
                                // 1: rows (i,l) i-major (levels_first, strided levels)
                                // 2: rows (l,i) l-major (levels_last)
     uint8_t lid64;
-    uint8_t pad1;
+    uint8_t fpol;              // field-side cache policy (as seg_s)
     uint32_t tile_bytes;
     uint8_t pad[8];
 };

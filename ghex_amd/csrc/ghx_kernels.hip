@@ -60,18 +60,73 @@ struct vec_t<1>
     using type = unsigned char;
 };
 
+// Fields and buffers are device (global) memory: address-space-1 pointers make the compiler
+// emit global_load/global_store instead of flat_* (no aperture check, and no lgkmcnt coupling
+// that forces every store to wait for all outstanding loads).
+#define GHX_GLOBAL __attribute__((address_space(1)))
+
 template<typename V, bool NTL>
 __device__ __forceinline__ V vload(const char* p)
 {
-    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
-    else return *reinterpret_cast<const V*>(p);
+    const GHX_GLOBAL V* g = (const GHX_GLOBAL V*)(p);
+    if constexpr (NTL) return __builtin_nontemporal_load(g);
+    else return *g;
 }
 
 template<typename V, bool NTS>
 __device__ __forceinline__ void vstore(char* p, V v)
 {
-    if constexpr (NTS) __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
-    else *reinterpret_cast<V*>(p) = v;
+    GHX_GLOBAL V* g = (GHX_GLOBAL V*)(p);
+    if constexpr (NTS) __builtin_nontemporal_store(v, g);
+    else *g = v;
+}
+
+// Field-side accesses under the segment's cache policy (seg_s::fpol, uniform per tile):
+// bit 0 = non-temporal load ("nt"), bit 1 = store with sc1 (gfx950 cache-policy bit; the
+// compiler exposes no builtin for it, hence the asm). Short rows are the request-bound part of a
+// halo; nt loads keep their 128-B line fills from allocating in the Infinity Cache, sc1 stores
+// issue each masked row write once (tools/cpol_bench.hip).
+template<typename V, bool NTL>
+__device__ __forceinline__ V fload(const char* p, uint32_t pol)
+{
+    if (!NTL && (pol & 1u)) return __builtin_nontemporal_load((const GHX_GLOBAL V*)(p));
+    return vload<V, NTL>(p);
+}
+
+template<typename V, bool NTS>
+__device__ __forceinline__ void fstore(char* p, V v, uint32_t pol)
+{
+    if constexpr (sizeof(V) == 16)
+    {
+        if (!NTS && (pol & 2u))
+        {
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+            return;
+        }
+    }
+    else if constexpr (sizeof(V) == 8)
+    {
+        if (!NTS && (pol & 2u))
+        {
+            asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+            return;
+        }
+    }
+    else if constexpr (sizeof(V) == 4)
+    {
+        if (!NTS && (pol & 2u))
+        {
+            asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+            return;
+        }
+    }
+    vstore<V, NTS>(p, v);
+}
+
+template<typename Seg>
+__device__ __forceinline__ uint32_t fpol_of(const Seg& s)
+{
+    return s.fpol;
 }
 
 // field byte offset of segment-relative buffer position p (structured)
@@ -91,8 +146,8 @@ __device__ __forceinline__ int64_t field_offset_s(const seg_s& s, uint32_t p)
 
 __device__ __forceinline__ int64_t load_lid(const seg_u& s, uint32_t i)
 {
-    if (s.lid64) return static_cast<const int64_t*>(s.lids)[i];
-    return static_cast<const int32_t*>(s.lids)[i];
+    if (s.lid64) return ((const GHX_GLOBAL int64_t*)(s.lids))[i];
+    return ((const GHX_GLOBAL int32_t*)(s.lids))[i];
 }
 
 // field byte offset of segment-relative buffer position p (unstructured: rows from lids)
@@ -142,6 +197,7 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
     constexpr bool NTL = NT >= 2;             // 2, 3: non-temporal loads
     constexpr bool NTS = NT == 1 || NT == 2;  // 1, 2: non-temporal stores
     const uint32_t tid = threadIdx.x;
+    const uint32_t pol = fpol_of(s);
     for (uint32_t base = start + tid * W; base < end; base += U * kBlock * W)
     {
         V v[U];
@@ -158,7 +214,7 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
             const uint32_t p = base + u * kBlock * W;
             if (p < end)
             {
-                if (PACK) v[u] = vload<V, NTL>(field + fo[u]);
+                if (PACK) v[u] = fload<V, NTL>(field + fo[u], pol);
                 else v[u] = vload<V, NTL>(buf + p);
             }
         }
@@ -169,7 +225,7 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
             if (p < end)
             {
                 if (PACK) vstore<V, NTS>(buf + p, v[u]);
-                else vstore<V, NTS>(field + fo[u], v[u]);
+                else fstore<V, NTS>(field + fo[u], v[u], pol);
             }
         }
     }

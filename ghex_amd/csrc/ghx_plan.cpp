@@ -41,6 +41,7 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
             tb -= tb % segs[i].row_bytes;  // whole rows per tile
         }
         segs[i].tile_bytes = tb;
+        segs[i].fpol = small ? uint8_t(g_tune.short_pol) : uint8_t(0);
         segs[i].first_tile = 0;
         const uint32_t nt = tiles_of(segs[i].bytes, tb);
         for (uint32_t t = 0; t < nt; ++t) per[i].push_back(t);

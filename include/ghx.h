@@ -46,7 +46,11 @@ typedef void* ghx_stream;
 /* Process-wide tuning knobs (development / benchmarking; defaults are the measured best):
  * "unroll" (2|4|8 vectors in flight per lane), "nt" (0 default cache policy, 1 non-temporal
  * stores, 2 non-temporal loads and stores), "grid_cap" (max workgroups, 0 = one per tile),
- * "tile_bytes" (buffer bytes per workgroup tile; applies to plans created afterwards).
+ * "tile_bytes" (buffer bytes per workgroup tile), "small_tile_rows", "small_row_bytes",
+ * "order" (0 segment order, 1 short-row segments first, 2 round-robin), "pair" (0|1),
+ * "short_pol" (field-side cache policy of short-row segments: bit 0 non-temporal loads,
+ * bit 1 sc1 stores); "reset" restores every default. Plan-shaping knobs apply to plans
+ * created afterwards.
  * No reference counterpart (the reference hard-codes block_dim=128, 1 element per thread:
  * include/ghex/structured/pack_kernels.hpp:211-214). */
 int ghx_tune(const char* key, int32_t value);

@@ -357,18 +357,16 @@ def test_full_size_512_h2_checksum():
 @pytest.mark.parametrize("knobs", [{"pair": 1}, {"pair": 1, "small_tile_rows": 64},
                                    {"order": 0, "small_tile_rows": 100, "unroll": 2},
                                    {"order": 2, "tile_bytes": 1024, "unroll": 8, "nt": 3},
-                                   {"grid_cap": 7, "nt": 1}])
+                                   {"grid_cap": 7, "nt": 1}, {"short_pol": 3},
+                                   {"short_pol": 1, "small_row_bytes": 4096}])
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_tuning_variants_stay_bit_exact(knobs, Hw):
     """Every launch/planning variant (ghx_tune) must produce the same bytes."""
     from ghex_amd import _ghx
-    defaults = dict(unroll=4, nt=0, grid_cap=0, tile_bytes=16384, small_tile_rows=4096,
-                    small_row_bytes=64, order=1, pair=0)
     try:
         for k, v in knobs.items():
             _ghx.call("ghx_tune", k.encode(), v)
         test_single_domain_periodic_fp64((2, 1, 0), Hw, 11)
         test_cube_multi_rank_emulated((2, 2, 2))
     finally:
-        for k, v in defaults.items():
-            _ghx.call("ghx_tune", k.encode(), v)
+        _ghx.call("ghx_tune", b"reset", 0)
