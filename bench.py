@@ -486,13 +486,13 @@ def bench_config4(torch, dev, ghex_amd, R):
 
 
 def bench_config5(torch, dev, _ghx, levels):
-    """BASELINE config 5 shape on one GPU: 10M cells (levels=1) / 2M cells (levels=8),
-    5 % halo, 7 peers, random lids (seed 20260715), levels_first fp64: fused gather of all
-    send lists + fused scatter of all recv lists (unstructured plans)."""
+    """BASELINE config 5 shape on one GPU: 10M cells, 5 % halo, 7 peers, random lids (seed
+    20260715), levels_first fp64: fused gather of all send lists + fused scatter of all recv
+    lists (unstructured plans)."""
     import ctypes
     import numpy as np
     rng = np.random.default_rng(20260715)
-    n = 10_000_000 if levels == 1 else 2_000_000
+    n = 10_000_000
     nh = n // 20
     send = rng.choice(n, size=nh, replace=False)
     recv = rng.permutation(n)[:nh]

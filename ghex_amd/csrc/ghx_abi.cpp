@@ -311,6 +311,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 1) throw invalid("pair must be 0 or 1");
             g_tune.pair = value;
         }
+        else if (k == "usort")
+        {
+            if (value < 0 || value > 1) throw invalid("usort must be 0 or 1");
+            g_tune.usort = value;
+        }
         else if (k == "short_pol")
         {
             if (value < 0 || value > 3) throw invalid("short_pol must be in 0..3");

@@ -39,6 +39,9 @@ struct tuning
                                        // y+1 share a cache line): one lane moves both. Off by
                                        // default: with short-row-first dispatch the L2 already
                                        // merges the shared-line misses (same TCC_EA0_RDREQ)
+    int usort = 0;                     // unstructured one-row-per-index segments: visit the
+                                       // indices in ascending field order (buffer side
+                                       // scattered through a permutation)
     int short_pol = 0;                 // field-side cache policy of short-row segments:
                                        // bit 0 non-temporal loads (pack), bit 1 sc1 stores
                                        // (unpack)
@@ -114,7 +117,7 @@ struct alignas(16) seg_u
     uint8_t lid64;
     uint8_t fpol;              // field-side cache policy (as seg_s)
     uint32_t tile_bytes;
-    uint8_t pad[8];
+    const uint32_t* perm;      // mode 0, sorted: lids ascending, perm[k] = buffer row of lid k
 };
 static_assert(sizeof(seg_u) == 96, "seg_u layout");
 

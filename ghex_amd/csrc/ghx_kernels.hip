@@ -174,6 +174,21 @@ __device__ __forceinline__ int64_t field_offset_u(const seg_u& s, uint32_t p)
     return load_lid(s, i) * s.index_stride_b + int64_t(l) * s.level_stride_b + int64_t(col);
 }
 
+// buffer byte position of segment-relative position p: p itself, except for sorted unstructured
+// segments (lids visited in ascending field order; perm maps back to the buffer row)
+__device__ __forceinline__ uint32_t buf_pos(const seg_s&, uint32_t p)
+{
+    return p;
+}
+
+__device__ __forceinline__ uint32_t buf_pos(const seg_u& s, uint32_t p)
+{
+    if (!s.perm) return p;
+    const uint32_t row = fastdiv(p, s.mag_row);
+    const uint32_t col = p - row * s.row_bytes;
+    return ((const GHX_GLOBAL uint32_t*)(s.perm))[row] * s.row_bytes + col;
+}
+
 template<typename Seg>
 __device__ __forceinline__ int64_t field_offset(const Seg& s, uint32_t p);
 template<>
@@ -202,20 +217,15 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
     {
         V v[U];
         int64_t fo[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-        {
-            const uint32_t p = base + u * kBlock * W;
-            if (p < end) fo[u] = field_offset<Seg>(s, p);
-        }
+        uint32_t bp[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
         {
             const uint32_t p = base + u * kBlock * W;
             if (p < end)
             {
-                if (PACK) v[u] = fload<V, NTL>(field + fo[u], pol);
-                else v[u] = vload<V, NTL>(buf + p);
+                fo[u] = field_offset<Seg>(s, p);
+                bp[u] = buf_pos(s, p);
             }
         }
 #pragma unroll
@@ -224,7 +234,17 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
             const uint32_t p = base + u * kBlock * W;
             if (p < end)
             {
-                if (PACK) vstore<V, NTS>(buf + p, v[u]);
+                if (PACK) v[u] = fload<V, NTL>(field + fo[u], pol);
+                else v[u] = vload<V, NTL>(buf + bp[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                if (PACK) vstore<V, NTS>(buf + bp[u], v[u]);
                 else fstore<V, NTS>(field + fo[u], v[u], pol);
             }
         }

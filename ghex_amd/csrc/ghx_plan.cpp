@@ -390,6 +390,8 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         int64_t n;
         bool wide;
         size_t off;
+        bool sorted = false;   // store lids ascending + the buffer-row permutation
+        size_t perm_off = 0;
     };
     std::vector<pending> pend;
     size_t lid_bytes = 0;
@@ -451,8 +453,17 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         if (s.mode != 0) w = std::min(w, wlog2_of(uint64_t(s.level_stride_b < 0 ? -s.level_stride_b : s.level_stride_b)));
         s.wlog2 = uint8_t(w);
         lid_bytes = (lid_bytes + 15) & ~size_t(15);
-        pend.push_back({segs.size(), en.lids, en.n_lids, wide, lid_bytes});
+        pending pe{segs.size(), en.lids, en.n_lids, wide, lid_bytes};
         lid_bytes += size_t(en.n_lids) * (wide ? 8 : 4);
+        if (g_tune.usort && s.mode == 0 && en.n_lids >= 256 &&
+            !std::is_sorted(en.lids, en.lids + en.n_lids))
+        {
+            lid_bytes = (lid_bytes + 15) & ~size_t(15);
+            pe.sorted = true;
+            pe.perm_off = lid_bytes;
+            lid_bytes += size_t(en.n_lids) * 4;
+        }
+        pend.push_back(pe);
         segs.push_back(s);
         bytes += uint64_t(total);
     }
@@ -464,17 +475,36 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         std::vector<unsigned char> host(lid_bytes);
         for (auto& p : pend)
         {
-            if (p.wide) std::memcpy(host.data() + p.off, p.lids, size_t(p.n) * 8);
+            std::vector<uint32_t> order;
+            if (p.sorted)
+            {
+                order.resize(size_t(p.n));
+                for (int64_t i = 0; i < p.n; ++i) order[size_t(i)] = uint32_t(i);
+                std::stable_sort(order.begin(), order.end(),
+                                 [&](uint32_t a, uint32_t b) { return p.lids[a] < p.lids[b]; });
+                std::memcpy(host.data() + p.perm_off, order.data(), size_t(p.n) * 4);
+            }
+            auto lid_at = [&](int64_t k) { return p.sorted ? p.lids[order[size_t(k)]] : p.lids[k]; };
+            if (p.wide)
+            {
+                int64_t* dst = reinterpret_cast<int64_t*>(host.data() + p.off);
+                for (int64_t i = 0; i < p.n; ++i) dst[i] = lid_at(i);
+            }
             else
             {
                 int32_t* dst = reinterpret_cast<int32_t*>(host.data() + p.off);
-                for (int64_t i = 0; i < p.n; ++i) dst[i] = int32_t(p.lids[i]);
+                for (int64_t i = 0; i < p.n; ++i) dst[i] = int32_t(lid_at(i));
             }
         }
         if (hipMalloc(&dev.lids, lid_bytes) != hipSuccess) throw hip_error("hipMalloc(lids)");
         if (hipMemcpy(dev.lids, host.data(), lid_bytes, hipMemcpyHostToDevice) != hipSuccess)
             throw hip_error("hipMemcpy(lids)");
-        for (auto& p : pend) segs[p.seg].lids = static_cast<char*>(dev.lids) + p.off;
+        for (auto& p : pend)
+        {
+            segs[p.seg].lids = static_cast<char*>(dev.lids) + p.off;
+            if (p.sorted)
+                segs[p.seg].perm = reinterpret_cast<const uint32_t*>(static_cast<char*>(dev.lids) + p.perm_off);
+        }
         void* keep = dev.lids;
         dev.lids = nullptr;  // upload() releases; re-attach after
         upload(dev, segs, tiles);

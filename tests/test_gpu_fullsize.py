@@ -71,15 +71,26 @@ def _random_lists(rng, n_cells, n_halo, peers):
     return np.split(send, cuts), np.split(rng.permutation(recv), cuts)
 
 
-@pytest.mark.parametrize("levels,levels_first", [(1, True), (8, True), (8, False), (3, False)])
-def test_config5_unstructured_10M(levels, levels_first):
-    """~10M cells, 5% halo, 7 peers; fused gather (pack) and scatter (unpack) of every peer's
-    index list vs the oracle's data_descriptor get/set, bit-exact."""
+@pytest.mark.parametrize("levels,levels_first,usort", [(1, True, 0), (1, True, 1), (8, True, 0),
+                                                      (8, True, 1), (8, False, 0), (3, False, 0)])
+def test_config5_unstructured_10M(levels, levels_first, usort):
+    """10M cells, 5% halo, 7 peers; fused gather (pack) and scatter (unpack) of every peer's
+    index list vs the oracle's data_descriptor get/set, bit-exact; usort=1 visits the indices in
+    ascending field order (buffer side through the permutation)."""
+    from ghex_amd import _ghx
+    _ghx.call("ghx_tune", b"usort", usort)
+    try:
+        _config5_case(levels, levels_first)
+    finally:
+        _ghx.call("ghx_tune", b"reset", 0)
+
+
+def _config5_case(levels, levels_first):
     import ctypes
     import torch
     from ghex_amd import _ghx
     rng = np.random.default_rng(20260715)
-    n = 10_000_000 if levels == 1 else 2_000_000
+    n = 10_000_000
     nh = n // 20
     sends, recvs = _random_lists(rng, n, nh, 7)
     vals = rng.random(n * levels)
