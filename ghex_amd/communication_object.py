@@ -11,6 +11,13 @@ exchange(buffer_infos):
      "nccl" = RCCL over xGMI), posted as one group (batch_isend_irecv), stream-ordered like the
      reference's stream-aware branch (:703-714, 751-765);
   4. ONE fused unpack launch for all recv buffers.
+
+staging="host" (the NIC-side path; arch_traits.hpp:51-75 keeps device buffers
+through oomph): after the pack, each peer send buffer is copied to a pinned host buffer (D2H on
+the exchange stream, one event per buffer so each host send starts as soon as its copy lands),
+messages travel over a gloo group between host buffers, and each received buffer is copied back
+(H2D) as soon as its message has arrived; the unpack launch is queued behind the copies.
+Self messages stay on the device exactly as in the default mode.
 """
 from __future__ import annotations
 
@@ -50,18 +57,20 @@ class _ExchangePlan:
             pass
 
 
-def route(context, sends, recvs):
+def route(context, sends, recvs, group=None):
     """Post one group of point-to-point messages. sends/recvs: [(peer_rank, tag, tensor)].
 
     Messages between one pair of ranks are matched in (tag) order on both sides (NCCL/RCCL
     matches by issue order; gloo by tag) — the tag of a send buffer equals the tag of the
-    matching recv buffer by construction of the pattern. Returns the list of works."""
+    matching recv buffer by construction of the pattern. Returns the list of works: the recvs
+    first, in (peer, tag) order, then the sends."""
     dist = context.distributed
+    group = context.group if group is None else group
     ops = []
     for peer, tag, t in sorted(recvs, key=lambda x: (x[0], x[1])):
-        ops.append(dist.P2POp(dist.irecv, t, context.global_rank(peer), context.group, tag))
+        ops.append(dist.P2POp(dist.irecv, t, context.global_rank(peer), group, tag))
     for peer, tag, t in sorted(sends, key=lambda x: (x[0], x[1])):
-        ops.append(dist.P2POp(dist.isend, t, context.global_rank(peer), context.group, tag))
+        ops.append(dist.P2POp(dist.isend, t, context.global_rank(peer), group, tag))
     if not ops:
         return []
     return dist.batch_isend_irecv(ops)
@@ -103,12 +112,24 @@ class CommunicationHandle:
 class CommunicationObject:
     """communication_object<grid, domain_id> (make_communication_object, :1105-1112)."""
 
-    def __init__(self, context, fuse_self: bool = True):
+    def __init__(self, context, fuse_self: bool = True, staging=None):
+        if staging not in (None, "host"):
+            raise ValueError("staging must be None (device buffers) or 'host'")
         self.context = context
         self.fuse_self = fuse_self
+        self.staging = staging
         self._plans = {}
         self._bufs = {}
+        self._host = {}
         self._valid = False
+        self._host_group = None
+        if staging == "host" and context.distributed is not None and context.size() > 1:
+            dist = context.distributed
+            if dist.get_backend(context.group) == "gloo":
+                self._host_group = context.group
+            else:  # a host-transport group over the same ranks (collective: every rank builds it)
+                ranks = None if context.group is None else dist.get_process_group_ranks(context.group)
+                self._host_group = dist.new_group(ranks=ranks, backend="gloo")
 
     def all_self(self, plan) -> bool:
         """Every message is a self message and libghx can fuse pack+unpack (ghx_exchange_self)."""
@@ -209,13 +230,56 @@ class CommunicationObject:
                  if x["rank"] != me]
         recvs = [(x["rank"], x["tag"], recv[i][:x["size"]]) for i, x in enumerate(plan.recv)
                  if x["rank"] != me]
-        for w in route(self.context, sends, recvs):
-            w.wait()  # stream-ordered for NCCL: the unpack below is queued behind the recvs
+        if self.staging == "host":
+            self._exchange_host_staged(plan, sends, recvs, stream)
+        else:
+            for w in route(self.context, sends, recvs):
+                w.wait()  # stream-ordered for NCCL: the unpack below is queued behind the recvs
         _ghx.call("ghx_exchange_unpack", plan.h, fptrs, len(bis), rptrs, len(recv),
                   stream.cuda_stream)
         ev = torch.cuda.Event()
         ev.record(stream)
         return CommunicationHandle(self, stream, ev)
+
+    def _host_buffers(self, plan, sends, recvs):
+        import torch
+        key = id(plan)
+        h = self._host.get(key)
+        if h is None:
+            h = ([torch.empty(t.numel(), dtype=torch.uint8, pin_memory=True) for _, _, t in sends],
+                 [torch.empty(t.numel(), dtype=torch.uint8, pin_memory=True) for _, _, t in recvs])
+            self._host[key] = h
+        return h
+
+    def _exchange_host_staged(self, plan, sends, recvs, stream):
+        """pack (queued) -> per-buffer D2H + event -> host sends as copies land; host recvs ->
+        per-buffer H2D as messages land; the caller queues the unpack behind the H2D copies."""
+        import torch
+        hs, hr = self._host_buffers(plan, sends, recvs)
+        evs = []
+        with torch.cuda.stream(stream):
+            for (_, _, t), h in zip(sends, hs):
+                h.copy_(t, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                evs.append(ev)
+        dist = self.context.distributed
+        group = self._host_group
+        rops = []
+        for (peer, tag, _), h in sorted(zip(recvs, hr), key=lambda x: (x[0][0], x[0][1])):
+            rops.append((dist.irecv(h, self.context.global_rank(peer), group, tag), h, peer, tag))
+        sops = []
+        for ((peer, tag, _), h), ev in sorted(zip(zip(sends, hs), evs),
+                                              key=lambda x: (x[0][0][0], x[0][0][1])):
+            ev.synchronize()
+            sops.append(dist.isend(h, self.context.global_rank(peer), group, tag))
+        dev_of = {(p, g): t for p, g, t in recvs}
+        with torch.cuda.stream(stream):
+            for w, h, peer, tag in rops:
+                w.wait()
+                dev_of[(peer, tag)].copy_(h, non_blocking=True)
+        for w in sops:
+            w.wait()
 
     # low-level access for benchmarks / tests (no transport)
     def pack_only(self, bis, stream=None):

@@ -1,0 +1,56 @@
+"""Worker for tests/test_gpu_multiproc.py: one rank of a real multi-process exchange, every rank
+on cuda:0 of the test box (RCCL needs one GPU per rank, so the transport here is gloo with
+host-staged buffers — the product's staging="host" mode). Launched with RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT in the environment; exits 0 when every cell of the rank's field
+(owned + halo) holds the wrapped global linear index after the exchange.
+
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    px, py, pz, N, Hw = (int(v) for v in sys.argv[1:6])
+    reps = int(sys.argv[6]) if len(sys.argv) > 6 else 3
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    assert world == px * py * pz
+    torch.cuda.set_device(0)
+    import ghex_amd
+    from ghex_amd.structured import regular as R
+    from tests import helpers as H
+    from tests.gpu_util import device_field
+    ghex_amd.native_library()
+    ranks, gf, gl = H.cube_domains(N, (px, py, pz))
+    dom = ranks[rank][0]
+    ctx = ghex_amd.make_context()
+    dd = R.DomainDescriptor(dom.id, dom.first, dom.last)
+    pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (True,) * 3), [dd])
+    bad = 0
+    for layout in [(2, 1, 0), (0, 2, 1)]:
+        a, _ = H.linear_index_field(dom, N, Hw, gl, layout=layout)
+        expect = H.expected_linear_halo(a, dom, N, Hw, gl, layout=layout)
+        base, logical = device_field(a, layout)
+        fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)
+        co = R.make_communication_object(ctx, staging="host")
+        for _ in range(reps):
+            co.exchange([pc(fd)]).wait()
+        got = base.cpu().numpy()
+        bad += int(np.count_nonzero(got != expect))
+    t = torch.tensor([bad])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(f"world {world} parts {(px, py, pz)} N {N} H {Hw}: bad cells {int(t.item())}")
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.exit(0 if int(t.item()) == 0 else 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,53 @@
+"""Real multi-process exchanges on the GPU: 2 and 4 ranks (separate processes, all on cuda:0),
+pack and unpack through libghx, peer messages over gloo between pinned host buffers
+(staging="host"), self messages on the device. Every cell of every rank is checked against the
+reference tests' halo property (wrapped global linear index). The workers are started as child
+processes (never exec'd over this one) and are bounded by a timeout."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("parts,N,Hw", [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)])
+def test_host_staged_exchange_multi_process(parts, N, Hw):
+    world = parts[0] * parts[1] * parts[2]
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), LOCAL_RANK="0")
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(HERE, "mp_exchange_worker.py"),
+             *map(str, parts), str(N), str(Hw)],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs, codes = [], []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+        codes.append(p.returncode)
+    assert codes == [0] * world, "\n".join(outs)
+    assert "bad cells 0" in outs[0]
