@@ -19,7 +19,7 @@ namespace ghx
 {
 // Bytes of buffer covered by one workgroup tile (default 256 threads x 4 vectors x 16 B); the
 // tile size is a plan-time tuning knob bounded by kMaxTileBytes.
-constexpr uint32_t kTileBytes = 16384;
+constexpr uint32_t kTileBytes = 8192;
 constexpr uint32_t kMaxTileBytes = 1u << 20;
 constexpr int kBlock = 256;
 

@@ -1,7 +1,7 @@
 // ghx_kernels.hip — gfx950 (CDNA4) pack / unpack kernels for the halo path.
 //
 // One launch covers every (field, iteration space, buffer) of a plan. Work is cut in the
-// BUFFER's byte space: a workgroup tile is tile_bytes (default 16 KiB) of one segment's buffer
+// BUFFER's byte space: a workgroup tile is tile_bytes (default 8 KiB) of one segment's buffer
 // range, so the buffer side is always a linear, fully coalesced 16 B/lane stream, and the field
 // side is linear within each contiguous row. Each lane decodes its buffer byte position into
 // (row, column) and the row into field coordinates with magic-number division, so no launch
