@@ -8,6 +8,8 @@ any compute entry point without it raises ImportError — there is no CPU fallba
 """
 from ._ghx import GhxError, LIB_PATH  # noqa: F401
 from .context import Context, make_context  # noqa: F401
+from .bulk_communication_object import (BulkCommunicationObject,  # noqa: F401
+                                        make_bulk_communication_object)
 
 __version__ = "0.1.0"
 

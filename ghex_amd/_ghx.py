@@ -89,6 +89,13 @@ _SIGS = {
     "ghx_exchange_unpack": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
     "ghx_exchange_self_fusable": (c_i32, [c_vp, P(c_i32)]),
     "ghx_exchange_self": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_ipc_export": (c_i32, [c_vp, P(ctypes.c_ubyte), P(ctypes.c_uint64)]),
+    "ghx_ipc_import": (c_i32, [P(ctypes.c_ubyte), ctypes.c_uint64, P(c_vp), P(c_vp)]),
+    "ghx_ipc_close": (c_i32, [c_vp]),
+    "ghx_put_create": (c_i32, [P(PackEntry), c_i32, P(PackEntry), c_i32, P(c_vp)]),
+    "ghx_put_execute": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_put_info": (c_i32, [c_vp, P(ctypes.c_uint64), P(c_i32)]),
+    "ghx_put_destroy": (c_i32, [c_vp]),
 }
 EXPORTED = tuple(_SIGS)
 

@@ -154,6 +154,29 @@ struct ghx_exchange : ghx::exchange_plan
 {
 };
 
+// Put plan: the pack plan of the source side and the unpack plan of the target side, segment k
+// of each covering the same virtual message bytes with the same tiling (checked).
+struct ghx_put
+{
+    std::unique_ptr<ghx::splan> from, to;
+    ghx_put(const ghx_pack_entry* src, int n_src, const ghx_pack_entry* dst, int n_dst)
+    : from(new ghx::splan(src, n_src, 0)), to(new ghx::splan(dst, n_dst, 1))
+    {
+        bool ok = from->host_segs.size() == to->host_segs.size() && from->n_tiles == to->n_tiles &&
+                  from->bytes == to->bytes;
+        for (size_t k = 0; ok && k < from->host_segs.size(); ++k)
+        {
+            const auto& a = from->host_segs[k];
+            const auto& b = to->host_segs[k];
+            ok = a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
+                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes;
+        }
+        if (!ok)
+            throw ghx::invalid("source and target iteration spaces do not describe the same "
+                               "message bytes (shapes, order, element sizes or row structure differ)");
+    }
+};
+
 using namespace ghx;
 
 namespace
@@ -790,6 +813,129 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
             a.buf_ptr[i] = reinterpret_cast<uint64_t>(buffers[i]);
         }
         return launch_self(a, stream, grid_for_tiles(p.n_tiles));
+    });
+}
+
+// ---------------------------------------------------------------------------------------------
+// zero-copy put (IPC + direct field-to-field copy)
+// ---------------------------------------------------------------------------------------------
+int ghx_ipc_export(const void* ptr, unsigned char handle[64], uint64_t* offset)
+{
+    return guarded([&] {
+        check_ptr(ptr, "ptr");
+        check_ptr(handle, "handle");
+        check_ptr(offset, "offset");
+        static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)) != hipSuccess)
+            throw hip_error("hipMemGetAddressRange");
+        hipIpcMemHandle_t h;
+        if (hipIpcGetMemHandle(&h, reinterpret_cast<void*>(base)) != hipSuccess)
+            throw hip_error("hipIpcGetMemHandle");
+        std::memcpy(handle, &h, sizeof(h));
+        *offset = uint64_t(static_cast<const char*>(ptr) - reinterpret_cast<const char*>(base));
+        return GHX_OK;
+    });
+}
+
+int ghx_ipc_import(const unsigned char handle[64], uint64_t offset, void** base, void** ptr)
+{
+    return guarded([&] {
+        check_ptr(handle, "handle");
+        check_ptr(base, "base");
+        check_ptr(ptr, "ptr");
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handle, sizeof(h));
+        void* b = nullptr;
+        if (hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+            throw hip_error("hipIpcOpenMemHandle");
+        *base = b;
+        *ptr = static_cast<char*>(b) + offset;
+        return GHX_OK;
+    });
+}
+
+int ghx_ipc_close(void* base)
+{
+    return guarded([&] {
+        check_ptr(base, "base");
+        if (hipIpcCloseMemHandle(base) != hipSuccess) throw hip_error("hipIpcCloseMemHandle");
+        return GHX_OK;
+    });
+}
+
+int ghx_put_create(const ghx_pack_entry* src, int32_t n_src, const ghx_pack_entry* dst,
+                   int32_t n_dst, ghx_put** out)
+{
+    return guarded([&] {
+        check_ptr(out, "out");
+        *out = nullptr;
+        if (n_src < 0 || n_dst < 0 || (n_src && !src) || (n_dst && !dst))
+            throw invalid("bad entry arrays");
+        const int saved_pair = g_tune.pair;
+        g_tune.pair = 0;  // partner segments have no counterpart on the other side
+        std::unique_ptr<ghx_put> p;
+        try
+        {
+            p.reset(new ghx_put(src, n_src, dst, n_dst));
+        }
+        catch (...)
+        {
+            g_tune.pair = saved_pair;
+            throw;
+        }
+        g_tune.pair = saved_pair;
+        *out = p.release();
+        return GHX_OK;
+    });
+}
+
+int ghx_put_execute(const ghx_put* put, void* const* src_fields, int32_t n_src,
+                    void* const* dst_fields, int32_t n_dst, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(put, "put");
+        const splan& p = *put->from;
+        const splan& q = *put->to;
+        if (p.n_tiles == 0) return int(GHX_OK);
+        if (n_src <= p.max_field_slot || n_dst <= q.max_field_slot)
+            throw invalid("pointer arrays do not cover the plan's slots");
+        if (!p.dev.segs || !q.dev.segs) throw hip_error("plan has no device tables");
+        kargs a{};
+        a.segs = p.dev.segs;
+        a.segs2 = q.dev.segs;
+        a.tile_seg = p.dev.tiles;
+        a.n_tiles = p.n_tiles;
+        for (int i = 0; i <= p.max_field_slot; ++i)
+        {
+            if (!src_fields[i]) throw invalid("null source field pointer");
+            a.field_ptr[i] = reinterpret_cast<uint64_t>(src_fields[i]);
+        }
+        for (int i = 0; i <= q.max_field_slot; ++i)
+        {
+            if (!dst_fields[i]) throw invalid("null target field pointer");
+            a.buf_ptr[i] = reinterpret_cast<uint64_t>(dst_fields[i]);
+        }
+        return launch_put(a, stream, grid_for_tiles(p.n_tiles));
+    });
+}
+
+int ghx_put_info(const ghx_put* put, uint64_t* bytes, int32_t* n_tiles)
+{
+    return guarded([&] {
+        check_ptr(put, "put");
+        if (bytes) *bytes = put->from->bytes;
+        if (n_tiles) *n_tiles = int32_t(put->from->n_tiles);
+        return GHX_OK;
+    });
+}
+
+int ghx_put_destroy(ghx_put* put)
+{
+    return guarded([&] {
+        delete put;
+        return GHX_OK;
     });
 }
 

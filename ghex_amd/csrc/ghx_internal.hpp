@@ -141,6 +141,7 @@ const char* get_error();
 int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid);
 int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid);
 int launch_self(const kargs& a, void* stream, uint32_t grid);
+int launch_put(const kargs& a, void* stream, uint32_t grid);
 uint32_t grid_for_tiles(uint32_t n_tiles);
 
 }  // namespace ghx

@@ -430,6 +430,67 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
     }
 }
 
+// Zero-copy put: element p of the virtual message is read from the source field through the
+// pack segment's addressing and written to the target field (peer memory or local) through the
+// unpack segment's addressing, register to register — no buffer.
+template<int W, int U>
+__device__ __forceinline__ void copy_direct(const seg_s& s, const seg_s& q,
+                                            const char* __restrict__ src, char* __restrict__ dst,
+                                            uint32_t start, uint32_t end)
+{
+    using V = typename vec_t<W>::type;
+    for (uint32_t base = start + threadIdx.x * W; base < end; base += U * kBlock * W)
+    {
+        V v[U];
+        int64_t fd[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end)
+            {
+                v[u] = vload<V, false>(src + field_offset_s(s, p));
+                fd[u] = field_offset_s(q, p);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * W;
+            if (p < end) vstore<V, false>(dst + fd[u], v[u]);
+        }
+    }
+}
+
+template<int U>
+__global__ __launch_bounds__(kBlock) void k_put(kargs a)
+{
+    const seg_s* __restrict__ ps = static_cast<const seg_s*>(a.segs);
+    const seg_s* __restrict__ qs = static_cast<const seg_s*>(a.segs2);
+    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
+    {
+        const uint32_t si = a.tile_seg[2 * t];
+        const uint32_t ti = a.tile_seg[2 * t + 1];
+        const seg_s s = ps[si];
+        const seg_s q = qs[si];
+        const uint32_t start = ti * s.tile_bytes;
+        const uint32_t end = min(start + s.tile_bytes, s.bytes);
+        const char* src = reinterpret_cast<const char*>(a.field_ptr[s.field_slot]);
+        char* dst = reinterpret_cast<char*>(a.buf_ptr[q.field_slot]);
+        int w = min(int(s.wlog2), int(q.wlog2));
+        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(src)));
+        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(dst)));
+        switch (w)
+        {
+            case 4: copy_direct<16, U>(s, q, src, dst, start, end); break;
+            case 3: copy_direct<8, U>(s, q, src, dst, start, end); break;
+            case 2: copy_direct<4, U>(s, q, src, dst, start, end); break;
+            case 1: copy_direct<2, U>(s, q, src, dst, start, end); break;
+            default: copy_direct<1, U>(s, q, src, dst, start, end); break;
+        }
+    }
+}
+
 template<typename Seg, bool PACK, int U>
 void launch_nt(const kargs& a, hipStream_t s, uint32_t grid)
 {
@@ -483,6 +544,22 @@ int launch_self(const kargs& a, void* stream, uint32_t grid)
     if (e != hipSuccess)
     {
         set_error(std::string("self-exchange kernel launch failed: ") + hipGetErrorString(e));
+        return GHX_ERR_HIP;
+    }
+    return GHX_OK;
+}
+
+int launch_put(const kargs& a, void* stream, uint32_t grid)
+{
+    if (a.n_tiles == 0) return GHX_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (g_tune.unroll == 8) hipLaunchKernelGGL((k_put<8>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (g_tune.unroll == 2) hipLaunchKernelGGL((k_put<2>), dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_put<4>), dim3(grid), dim3(kBlock), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+    {
+        set_error(std::string("put kernel launch failed: ") + hipGetErrorString(e));
         return GHX_ERR_HIP;
     }
     return GHX_OK;

@@ -285,6 +285,37 @@ int ghx_exchange_self_fusable(const ghx_exchange* ex, int32_t* fusable);
 int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
                       void* const* buffers, int32_t n_buffers, ghx_stream stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Zero-copy put between node-local GPUs. Replaces the reference's RMA path:
+ * bulk_communication_object (include/ghex/bulk_communication_object.hpp:206-704), the
+ * gpu_to_gpu put (include/ghex/structured/rma_put.hpp:204-245: one launch per range, one
+ * element per thread) and the CUDA IPC handles (include/ghex/rma/cuda/handle.hpp:20-96).
+ * ------------------------------------------------------------------------------------------ */
+
+/* Export the device allocation holding `ptr` for another process: a 64-byte IPC handle of the
+ * allocation's base and the byte offset of `ptr` inside it (torch's caching allocator hands out
+ * interior pointers). */
+int ghx_ipc_export(const void* ptr, unsigned char handle[64], uint64_t* offset);
+/* Map another process's allocation: *base is what ghx_ipc_close releases, *ptr = base+offset. */
+int ghx_ipc_import(const unsigned char handle[64], uint64_t offset, void** base, void** ptr);
+int ghx_ipc_close(void* base);
+
+/* A put plan: src[k] and dst[k] describe the two ends of the same virtual message bytes — the
+ * iteration spaces of a sender's send halo (its local coordinates, its field) and of the
+ * receiver's recv halo for the same key (the receiver's coordinates and field), each entry's
+ * buffer_slot/buffer_offset placing it in a virtual message exactly as ghx_plan_create would.
+ * Field slots: src entries index src_fields, dst entries index dst_fields (<= 64 each).
+ * Execution copies every element straight from the source field into the target field (peer
+ * memory through ghx_ipc_import, or the same device): no buffer, one launch. Fails with
+ * GHX_ERR_INVALID when the two sides do not describe the same bytes. */
+typedef struct ghx_put ghx_put;
+int ghx_put_create(const ghx_pack_entry* src, int32_t n_src, const ghx_pack_entry* dst,
+                   int32_t n_dst, ghx_put** out);
+int ghx_put_execute(const ghx_put* put, void* const* src_fields, int32_t n_src,
+                    void* const* dst_fields, int32_t n_dst, ghx_stream stream);
+int ghx_put_info(const ghx_put* put, uint64_t* bytes, int32_t* n_tiles);
+int ghx_put_destroy(ghx_put* put);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,7 +4,11 @@ host-staged buffers — the product's staging="host" mode). Launched with RANK /
 MASTER_ADDR / MASTER_PORT in the environment; exits 0 when every cell of the rank's field
 (owned + halo) holds the wrapped global linear index after the exchange.
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges]"""
+With mode "bulk" the exchange is the zero-copy BulkCommunicationObject instead: every rank puts
+its send regions straight into the peers' fields through IPC mappings (same GPU here, peer
+GPUs over xGMI on a multi-GPU node).
+
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk]"""
 import os
 import sys
 
@@ -15,6 +19,7 @@ sys.path.insert(0, ROOT)
 def main():
     px, py, pz, N, Hw = (int(v) for v in sys.argv[1:6])
     reps = int(sys.argv[6]) if len(sys.argv) > 6 else 3
+    mode = sys.argv[7] if len(sys.argv) > 7 else "staged"
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -38,16 +43,23 @@ def main():
         expect = H.expected_linear_halo(a, dom, N, Hw, gl, layout=layout)
         base, logical = device_field(a, layout)
         fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)
-        co = R.make_communication_object(ctx, staging="host")
-        for _ in range(reps):
-            co.exchange([pc(fd)]).wait()
+        if mode == "bulk":
+            co = ghex_amd.make_bulk_communication_object(ctx)
+            co.add_field(pc(fd))
+            for _ in range(reps):
+                co.exchange().wait()
+        else:
+            co = R.make_communication_object(ctx, staging="host")
+            for _ in range(reps):
+                co.exchange([pc(fd)]).wait()
         got = base.cpu().numpy()
         bad += int(np.count_nonzero(got != expect))
     t = torch.tensor([bad])
     dist.all_reduce(t)
     if rank == 0:
-        print(f"world {world} parts {(px, py, pz)} N {N} H {Hw}: bad cells {int(t.item())}")
+        print(f"{mode} world {world} parts {(px, py, pz)} N {N} H {Hw}: bad cells {int(t.item())}")
     dist.barrier()
+    del co
     dist.destroy_process_group()
     sys.exit(0 if int(t.item()) == 0 else 1)
 

@@ -1,6 +1,6 @@
-"""Real multi-process exchanges on the GPU: 2 and 4 ranks (separate processes, all on cuda:0),
-pack and unpack through libghx, peer messages over gloo between pinned host buffers
-(staging="host"), self messages on the device. Every cell of every rank is checked against the
+"""Real multi-process exchanges on the GPU: 2 and 4 ranks (separate processes, all on cuda:0):
+pack and unpack through libghx with peer messages over gloo between pinned host buffers
+(staging="host"), or zero-copy puts into the peers' fields through IPC mappings (bulk). Every cell of every rank is checked against the
 reference tests' halo property (wrapped global linear index). The workers are started as child
 processes (never exec'd over this one) and are bounded by a timeout."""
 import os
@@ -27,8 +27,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
+@pytest.mark.parametrize("mode", ["staged", "bulk"])
 @pytest.mark.parametrize("parts,N,Hw", [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)])
-def test_host_staged_exchange_multi_process(parts, N, Hw):
+def test_exchange_multi_process(parts, N, Hw, mode):
+    """staged: CommunicationObject(staging="host") over gloo; bulk: zero-copy IPC puts."""
     world = parts[0] * parts[1] * parts[2]
     port = _free_port()
     procs = []
@@ -37,7 +39,7 @@ def test_host_staged_exchange_multi_process(parts, N, Hw):
                    MASTER_PORT=str(port), LOCAL_RANK="0")
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(HERE, "mp_exchange_worker.py"),
-             *map(str, parts), str(N), str(Hw)],
+             *map(str, parts), str(N), str(Hw), "3", mode],
             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs, codes = [], []
     for p in procs:

@@ -204,3 +204,43 @@ def test_exchange_buffer_plan_matches_oracle():
         # 4-byte fields after 8-byte ones: the padding rule produced odd offsets somewhere?
         sizes = [b["size"] for b in plan.send]
         assert len(sizes) == 7
+
+
+def _put_entries(lasts, strides=(8, 96, 1152)):
+    import ctypes
+    from ghex_amd import _ghx
+    out = []
+    for last in lasts:
+        d = _ghx.FieldDesc()
+        d.dim, d.elem_size = 3, 8
+        for k in range(3):
+            d.layout[k] = 2 - k
+            d.byte_strides[k] = strides[k]
+            d.offsets[k] = 2
+            d.extents[k] = 12
+        d.num_components, d.has_components = 1, 0
+        arr = (_ghx.Box * 1)()
+        for k in range(3):
+            arr[0].first[k], arr[0].last[k] = 0, last[k]
+        e = _ghx.PackEntry()
+        e.field, e.field_slot, e.buffer_slot, e.buffer_offset = d, 0, 0, 0
+        e.boxes, e.n_boxes = ctypes.cast(arr, ctypes.POINTER(_ghx.Box)), 1
+        out.append((e, arr))
+    return out
+
+
+def test_put_plan_pairs_matching_sides_and_refuses_mismatch():
+    """ghx_put_create (zero-copy put, host-side planning only here): same message bytes on both
+    sides -> a plan; different shapes -> GHX_ERR_INVALID with a message."""
+    import ctypes
+    from ghex_amd import _ghx
+    L = _ghx.lib()
+    (a, ka), (b, kb) = _put_entries([(3, 1, 1), (3, 1, 1)])
+    h = ctypes.c_void_p()
+    assert L.ghx_put_create(ctypes.byref(a), 1, ctypes.byref(b), 1, ctypes.byref(h)) == 0
+    nb = ctypes.c_uint64()
+    assert L.ghx_put_info(h, ctypes.byref(nb), None) == 0 and nb.value == 4 * 2 * 2 * 8
+    assert L.ghx_put_destroy(h) == 0
+    (a, ka), (b, kb) = _put_entries([(3, 1, 1), (1, 3, 1)])
+    assert L.ghx_put_create(ctypes.byref(a), 1, ctypes.byref(b), 1, ctypes.byref(h)) == -1
+    assert b"same message bytes" in L.ghx_last_error()
