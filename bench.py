@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     p.add_argument("--tune", default="", help="developer: ghx_tune key=value,... before planning")
+    p.add_argument("--bulk", action="store_true",
+                   help="N>1: also time the zero-copy bulk exchange (IPC puts into peer halos); "
+                        "always on at N=1 (self puts)")
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the nccl process group even at world size 1 (path test)")
     return p.parse_args()
@@ -277,6 +280,31 @@ def main():
             co.exchange(bis).wait()
         Te = timed(lambda: co.exchange(bis).wait(), ke)
         out["exchange_ms_per_step"] = round(Te / ke * 1e3, 4)
+        if world == 1 or args.bulk:
+            # zero-copy bulk exchange (BulkCommunicationObject): puts straight into the
+            # receivers' halos, no buffers: 2*n*8 bytes moved per step (not the metric's 4*n*8)
+            try:
+                bco = ghex_amd.make_bulk_communication_object(ctx)
+                bco.add_field(bis[0])
+                bco.init()
+                for _ in range(3):
+                    bco.exchange().wait()
+                Tb = timed(lambda: bco.exchange().wait(), ke)
+                put = bco._puts[0]
+
+                def put_fn(s):
+                    rc = L.ghx_put_execute(put[0], put[1], put[2], put[3], put[4], s)
+                    if rc:
+                        raise RuntimeError(L.ghx_last_error().decode())
+                (t_put,) = kernel_durations(torch, dev, stream, [put_fn])
+                out["bulk"] = {"exchange_ms_per_step": round(Tb / ke * 1e3, 4),
+                               "put_launches": len(bco._puts),
+                               "put_us": round(t_put * 1e6, 2) if len(bco._puts) == 1 else None,
+                               "bytes_moved_per_step": 2 * n_halo * 8}
+                del bco
+            except Exception as e:  # reported, never fatal for the headline measurement
+                out["bulk"] = {"error": str(e)[:200]}
+            co.exchange(bis).wait()
         # host-staged: pack -> D2H (pinned) -> H2D -> unpack (NIC-side buffers, north star)
         hs = [torch.empty(b["size"], dtype=torch.uint8, pin_memory=True) for b in plan.send]
 

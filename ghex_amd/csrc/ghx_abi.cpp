@@ -169,7 +169,9 @@ struct ghx_put
             const auto& a = from->host_segs[k];
             const auto& b = to->host_segs[k];
             ok = a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
-                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes;
+                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes &&
+                 a.n_outer == b.n_outer;
+            for (int d = 0; ok && d < 4; ++d) ok = a.ext[d] == b.ext[d];
         }
         if (!ok)
             throw ghx::invalid("source and target iteration spaces do not describe the same "
