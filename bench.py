@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     p.add_argument("--tune", default="", help="developer: ghx_tune key=value,... before planning")
+    p.add_argument("--cold", action="store_true",
+                   help="also time the dominant launch right after a 1 GiB cache-flushing kernel "
+                        "(opt-in: its launches would skew a profiler's per-kernel average)")
     p.add_argument("--bulk", action="store_true",
                    help="N>1: also time the zero-copy bulk exchange (IPC puts into peer halos); "
                         "always on at N=1 (self puts)")
@@ -330,7 +333,7 @@ def main():
             # restore valid halos after the staged copies
             co.exchange(bis).wait()
 
-    if not args.no_extras:
+    if args.cold:
         # the dominant launch with cold caches: an application's stencil sweeps the whole field
         # between exchanges, so its halo rows are not left in the 256 MiB Infinity Cache as
         # they are when the bench replays exchanges back to back. A 1 GiB read-modify-write

@@ -336,6 +336,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 1) throw invalid("pair must be 0 or 1");
             g_tune.pair = value;
         }
+        else if (k == "u_tile_rows")
+        {
+            if (value < 1) throw invalid("u_tile_rows must be >= 1");
+            g_tune.u_tile_rows = uint32_t(value);
+        }
         else if (k == "usort")
         {
             if (value < 0 || value > 1) throw invalid("usort must be 0 or 1");

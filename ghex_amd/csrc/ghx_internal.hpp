@@ -32,6 +32,7 @@ struct tuning
     uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
     uint32_t small_tile_rows = 4096;   // rows per tile of segments with short rows
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
+    uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
     int order = 1;                     // tile dispatch order: 0 segment order, 1 short-row
                                        // segments first, 2 round-robin over segments
     int pair = 0;                      // pair short-row segments whose rows interleave in

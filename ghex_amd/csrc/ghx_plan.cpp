@@ -6,6 +6,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 #include "ghx_plan.hpp"
 
@@ -36,7 +37,11 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
         uint32_t tb = g_tune.tile_bytes;
         if (small)
         {
-            const uint64_t want = uint64_t(g_tune.small_tile_rows) * segs[i].row_bytes;
+            // structured short rows: few large tiles (measured best: 4096 rows); index-list
+            // gathers are latency-bound random accesses and want many workgroups in flight
+            const uint32_t rows = std::is_same<Seg, seg_u>::value ? g_tune.u_tile_rows
+                                                                  : g_tune.small_tile_rows;
+            const uint64_t want = uint64_t(rows) * segs[i].row_bytes;
             tb = uint32_t(std::max<uint64_t>(segs[i].row_bytes, std::min<uint64_t>(want, kMaxTileBytes)));
             tb -= tb % segs[i].row_bytes;  // whole rows per tile
         }

@@ -47,6 +47,8 @@ typedef void* ghx_stream;
  * "unroll" (2|4|8 vectors in flight per lane), "nt" (0 default cache policy, 1 non-temporal
  * stores, 2 non-temporal loads and stores), "grid_cap" (max workgroups, 0 = one per tile),
  * "tile_bytes" (buffer bytes per workgroup tile), "small_tile_rows", "small_row_bytes",
+ * "u_tile_rows" (rows per tile of short-row index-list segments), "usort" (0|1: visit index
+ * lists in ascending field order),
  * "order" (0 segment order, 1 short-row segments first, 2 round-robin), "pair" (0|1),
  * "short_pol" (field-side cache policy of short-row segments: bit 0 non-temporal loads,
  * bit 1 sc1 stores); "reset" restores every default. Plan-shaping knobs apply to plans

@@ -2,6 +2,7 @@
 """Copy the judged rocprofv3 summaries of a round from gpurun_out/prof_<round>/ into profiles/:
 
   profiles/<round>_bench_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `python3 bench.py`
+  profiles/<round>_bench_kernels_by_grid.csv  the same trace per (kernel, workgroup count)
   profiles/<round>_h{1,3}_kernel_stats.csv  the same at halo 1 / 3
   profiles/<round>_pmc.json                 per-kernel counters + corrected HBM bytes per launch
   profiles/pmc_traffic.json                 what bench.py reads for roofline.traffic
@@ -34,6 +35,26 @@ def main(rn):
     if line:
         with open(os.path.join(dst, f"{rn}_bench.json"), "w") as fh:
             fh.write(line[-1])
+    # per (kernel, workgroups) durations from the kernel trace: the bench's extras launch the
+    # same kernels on other plans (config 4, config 5, put), so the headline launch is the
+    # k_self / k_copy row with the 512^3 plan's grid
+    kt = os.path.join(src, "bench", "kt_kernel_trace.csv")
+    if os.path.exists(kt):
+        import collections
+        import csv
+        import re
+        acc = collections.defaultdict(list)
+        for r in csv.DictReader(open(kt)):
+            m = re.search(r"(k_\w+<[^>]*>)", r["Kernel_Name"])
+            if m:
+                acc[(m.group(1), int(r["Grid_Size_X"]) // 256)].append(
+                    int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        with open(os.path.join(dst, f"{rn}_bench_kernels_by_grid.csv"), "w") as fh:
+            fh.write("kernel,workgroups,calls,avg_ns,median_ns,min_ns,max_ns\n")
+            for (k, wg), v in sorted(acc.items()):
+                v.sort()
+                fh.write(f"\"{k}\",{wg},{len(v)},{sum(v) / len(v):.0f},{v[len(v) // 2]},"
+                         f"{v[0]},{v[-1]}\n")
     pmc, traffic = {}, {}
     for h in (1, 2, 3):
         d = os.path.join(src, f"pmc_h{h}")
