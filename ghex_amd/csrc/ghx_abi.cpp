@@ -10,6 +10,7 @@
 #include <new>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "ghx_pattern.hpp"
 #include "ghx_plan.hpp"
@@ -101,6 +102,80 @@ class plan_cache
 plan_cache& cache()
 {
     static plan_cache c;
+    return c;
+}
+
+// Plan cache for ghx_unstructured_pack/unpack. Index lists can be long (10^5-10^6), so the key
+// is (descriptor, list address, length, index width, direction) plus an FNV-1a fingerprint of
+// up to 256 evenly spaced entries — the reference's pattern keeps its lid vectors alive and
+// unchanged for its lifetime (include/ghex/unstructured/pattern.hpp:53-90), which is the
+// contract here too.
+class uplan_cache
+{
+    std::mutex mtx_;
+    std::list<std::string> lru_;
+    std::unordered_map<std::string, std::pair<std::unique_ptr<uplan>, std::list<std::string>::iterator>> map_;
+    static constexpr size_t kCap = 256;
+
+  public:
+    const uplan* get(const ghx_udata_desc& d, const void* lids, int32_t lid_bytes, int64_t n, int dir)
+    {
+        uint64_t fp = 1469598103934665603ULL;
+        const int64_t step = n > 256 ? n / 256 : 1;
+        for (int64_t i = 0; i < n; i += step)
+        {
+            const int64_t v = lid_bytes == 8 ? static_cast<const int64_t*>(lids)[i]
+                                             : static_cast<const int32_t*>(lids)[i];
+            fp = (fp ^ uint64_t(v)) * 1099511628211ULL;
+        }
+        if (n > 0)
+        {
+            const int64_t v = lid_bytes == 8 ? static_cast<const int64_t*>(lids)[n - 1]
+                                             : static_cast<const int32_t*>(lids)[n - 1];
+            fp = (fp ^ uint64_t(v)) * 1099511628211ULL;
+        }
+        std::string key(reinterpret_cast<const char*>(&d), sizeof(d));
+        const uint64_t meta[5] = {uint64_t(reinterpret_cast<uintptr_t>(lids)), uint64_t(n),
+                                  uint64_t(lid_bytes), uint64_t(dir), fp};
+        key.append(reinterpret_cast<const char*>(meta), sizeof(meta));
+        std::lock_guard<std::mutex> lk(mtx_);
+        auto it = map_.find(key);
+        if (it != map_.end())
+        {
+            lru_.splice(lru_.begin(), lru_, it->second.second);
+            return it->second.first.get();
+        }
+        std::vector<int64_t> wide;
+        const int64_t* l64 = static_cast<const int64_t*>(lids);
+        if (lid_bytes == 4)
+        {
+            wide.resize(size_t(n));
+            for (int64_t i = 0; i < n; ++i) wide[size_t(i)] = static_cast<const int32_t*>(lids)[i];
+            l64 = wide.data();
+        }
+        ghx_upack_entry e{};
+        e.data = d;
+        e.field_slot = 0;
+        e.buffer_slot = 0;
+        e.buffer_offset = 0;
+        e.lids = l64;
+        e.n_lids = n;
+        auto p = std::make_unique<uplan>(&e, 1, dir);
+        if (map_.size() >= kCap)
+        {
+            (void)hipDeviceSynchronize();  // evicted plans may still be in flight
+            map_.erase(lru_.back());
+            lru_.pop_back();
+        }
+        lru_.push_front(key);
+        const uplan* raw = p.get();
+        map_.emplace(key, std::make_pair(std::move(p), lru_.begin()));
+        return raw;
+    }
+};
+uplan_cache& ucache()
+{
+    static uplan_cache c;
     return c;
 }
 }  // namespace
@@ -437,6 +512,36 @@ int ghx_structured_unpack(const ghx_field_desc* field, void* field_data, const v
         if (n_boxes < 0 || (n_boxes > 0 && !boxes)) throw invalid("bad boxes");
         const splan* p = cache().get(*field, boxes, n_boxes, 1);
         void* f[1] = {field_data};
+        void* b[1] = {const_cast<void*>(buffer)};
+        return p->execute(f, 1, b, 1, stream);
+    });
+}
+
+int ghx_unstructured_pack(const ghx_udata_desc* data, const void* values, void* buffer,
+                          const void* lids, int32_t lid_bytes, int64_t n_lids, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(data, "data");
+        if (lid_bytes != 4 && lid_bytes != 8) throw invalid("lid_bytes must be 4 or 8");
+        if (n_lids < 0 || (n_lids > 0 && !lids)) throw invalid("bad index list");
+        if (n_lids == 0) return int(GHX_OK);
+        const uplan* p = ucache().get(*data, lids, lid_bytes, n_lids, 0);
+        void* f[1] = {const_cast<void*>(values)};
+        void* b[1] = {buffer};
+        return p->execute(f, 1, b, 1, stream);
+    });
+}
+
+int ghx_unstructured_unpack(const ghx_udata_desc* data, void* values, const void* buffer,
+                            const void* lids, int32_t lid_bytes, int64_t n_lids, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(data, "data");
+        if (lid_bytes != 4 && lid_bytes != 8) throw invalid("lid_bytes must be 4 or 8");
+        if (n_lids < 0 || (n_lids > 0 && !lids)) throw invalid("bad index list");
+        if (n_lids == 0) return int(GHX_OK);
+        const uplan* p = ucache().get(*data, lids, lid_bytes, n_lids, 1);
+        void* f[1] = {values};
         void* b[1] = {const_cast<void*>(buffer)};
         return p->execute(f, 1, b, 1, stream);
     });

@@ -1,0 +1,134 @@
+// ghex_amd/data_descriptor.hpp — header-only C++ adaptor: GHEX's unstructured data-descriptor
+// concept on top of the C ABI of libghx.so (include/ghx.h).
+//
+// Replaces ghex::unstructured::data_descriptor<ghex::gpu, DomainId, Idx, T>
+// (include/ghex/unstructured/user_concepts.hpp:526-667): same constructor arguments, same
+// queries (domain_id(), domain_size(), num_components(), levels_first(), data(),
+// device_id()), and the concept's
+//     pack(T* buffer, const IndexContainer& c, void* stream_ptr)
+//     unpack(const T* buffer, const IndexContainer& c, void* stream_ptr)
+// where IndexContainer is a range of iteration spaces with `.local_indices()` (a host-readable
+// contiguous vector of 4- or 8-byte integer local ids, ghex's
+// unstructured::pattern::iteration_space, include/ghex/unstructured/pattern.hpp:53-90). As in
+// the reference, the buffer is NOT advanced between iteration spaces (there is exactly one per
+// neighbour, unstructured/pattern.hpp:324-325). Each list becomes one fused libghx launch with
+// the indices resident in device memory (the reference reads them from managed memory).
+//
+// Depends only on <ghx.h> and the standard library; link with -lghx.
+#pragma once
+
+#include <ghx.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+namespace ghex_amd
+{
+namespace unstructured
+{
+inline void check_u(int rc, const char* what)
+{
+    if (rc != GHX_OK)
+        throw std::runtime_error(std::string(what) + " failed: " + ghx_last_error());
+}
+
+template<typename DomainId, typename T>
+class data_descriptor
+{
+  public:  // member types (user_concepts.hpp:529-533)
+    using value_type = T;
+    using domain_id_type = DomainId;
+    using device_id_type = int;
+
+  private:
+    domain_id_type m_domain_id;
+    std::size_t m_domain_size;
+    int m_levels;
+    bool m_levels_first;
+    std::size_t m_index_stride;
+    std::size_t m_level_stride;
+    value_type* m_values;
+    device_id_type m_device_id;
+    ghx_udata_desc m_desc{};
+
+  public:
+    /** values: device pointer to domain_size * levels elements (plus padding when
+     * outer_stride is given); levels_first: levels of one index are contiguous; outer_stride:
+     * distance between consecutive indices (levels_first) or levels (levels last), 0 = dense.
+     * (user_concepts.hpp:547-566) */
+    template<typename Domain>
+    data_descriptor(const Domain& domain, value_type* values, int levels = 1,
+                    bool levels_first = true, std::size_t outer_stride = 0, device_id_type device_id = 0)
+    : data_descriptor(domain.domain_id(), domain.size(), values, levels, levels_first,
+                      outer_stride, device_id)
+    {
+    }
+
+    data_descriptor(domain_id_type domain_id, std::size_t domain_size, value_type* values,
+                    int levels = 1, bool levels_first = true, std::size_t outer_stride = 0,
+                    device_id_type device_id = 0)
+    : m_domain_id{domain_id}
+    , m_domain_size{domain_size}
+    , m_levels{levels}
+    , m_levels_first{levels_first}
+    , m_index_stride{levels_first ? (outer_stride ? outer_stride : std::size_t(levels)) : 1u}
+    , m_level_stride{levels_first ? 1u : (outer_stride ? outer_stride : domain_size)}
+    , m_values{values}
+    , m_device_id{device_id}
+    {
+        if (levels < 1) throw std::runtime_error("levels must be >= 1");
+        m_desc.elem_size = int32_t(sizeof(T));
+        m_desc.levels = levels;
+        m_desc.levels_first = levels_first ? 1 : 0;
+        m_desc.index_stride = int64_t(m_index_stride);
+        m_desc.level_stride = int64_t(m_level_stride);
+    }
+
+    domain_id_type domain_id() const noexcept { return m_domain_id; }
+    std::size_t domain_size() const noexcept { return m_domain_size; }
+    int num_components() const noexcept { return m_levels; }
+    bool levels_first() const noexcept { return m_levels_first; }
+    value_type* data() const noexcept { return m_values; }
+    device_id_type device_id() const noexcept { return m_device_id; }
+    const ghx_udata_desc& desc() const noexcept { return m_desc; }
+
+    template<typename IndexContainer>
+    void pack(value_type* buffer, const IndexContainer& c, void* stream_ptr)
+    {
+        for (const auto& is : c)
+        {
+            const auto& l = is.local_indices();
+            check_u(ghx_unstructured_pack(&m_desc, m_values, buffer, l.data(), lid_bytes(l),
+                                          int64_t(l.size()), stream_of(stream_ptr)),
+                    "ghx_unstructured_pack");
+        }
+    }
+
+    template<typename IndexContainer>
+    void unpack(const value_type* buffer, const IndexContainer& c, void* stream_ptr)
+    {
+        for (const auto& is : c)
+        {
+            const auto& l = is.local_indices();
+            check_u(ghx_unstructured_unpack(&m_desc, m_values, buffer, l.data(), lid_bytes(l),
+                                            int64_t(l.size()), stream_of(stream_ptr)),
+                    "ghx_unstructured_unpack");
+        }
+    }
+
+  private:
+    template<typename V>
+    static int32_t lid_bytes(const V&)
+    {
+        using I = std::decay_t<decltype(*std::declval<const V&>().data())>;
+        static_assert(std::is_integral<I>::value && (sizeof(I) == 4 || sizeof(I) == 8),
+                      "local indices must be 4- or 8-byte integers");
+        return int32_t(sizeof(I));
+    }
+
+    static ghx_stream stream_of(void* arg) { return arg ? *static_cast<ghx_stream*>(arg) : nullptr; }
+};
+}  // namespace unstructured
+}  // namespace ghex_amd

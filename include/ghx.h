@@ -166,6 +166,18 @@ typedef struct ghx_upack_entry
 
 typedef struct ghx_uplan ghx_uplan;
 
+/* The reference's data_descriptor<gpu>::pack/unpack(T* buffer, const IndexContainer& c, void*
+ * stream) for ONE index list (include/ghex/unstructured/user_concepts.hpp:583-666): gather
+ * values[lids[i]] (all levels, the descriptor's layout) into `buffer` / scatter back. `lids` is
+ * a HOST-readable array of int32 (lid_bytes 4) or int64 (8) local indices, e.g. the pattern's
+ * iteration_space::local_indices(). Plans are cached by (descriptor, list address, length, a
+ * fingerprint of the entries): the list must stay unchanged while it is in use, as the
+ * reference's pattern keeps it. */
+int ghx_unstructured_pack(const ghx_udata_desc* data, const void* values, void* buffer,
+                          const void* lids, int32_t lid_bytes, int64_t n_lids, ghx_stream stream);
+int ghx_unstructured_unpack(const ghx_udata_desc* data, void* values, const void* buffer,
+                            const void* lids, int32_t lid_bytes, int64_t n_lids, ghx_stream stream);
+
 /* Fused unstructured pack (0) / unpack (1) plan: replaces data_descriptor<gpu>::pack/unpack
  * and the four pack/unpack_kernel_levels_{first,last} launches per neighbour
  * (include/ghex/unstructured/user_concepts.hpp:455-523, 583-666). Index lists live in
