@@ -77,7 +77,8 @@ def route(context, sends, recvs, group=None):
 
 
 class CommunicationHandle:
-    """communication_handle (communication_object.hpp:78-130): wait / is_ready / progress."""
+    """communication_handle (communication_object.hpp:78-130): wait / is_ready / progress /
+    schedule_wait."""
 
     def __init__(self, co, stream, event):
         self._co = co
@@ -85,13 +86,20 @@ class CommunicationHandle:
         self._event = event
 
     def wait(self):
-        if self._event is not None:
+        co, self._co = self._co, None
+        if co is not None and co.has_scheduled_exchange():
+            co.complete_schedule_exchange()  # (:810-819) syncs the schedule_wait stream
+        elif self._event is not None:
             self._event.synchronize()
-        if self._co is not None:
-            self._co._valid = False
-            self._co = None
+        if co is not None:
+            co._valid = False
 
     def is_ready(self) -> bool:
+        if self._co is not None and self._co.has_scheduled_exchange():
+            if not self._co._scheduled_event.query():
+                return False
+            self.wait()
+            return True
         if self._event is None or self._event.query():
             if self._co is not None:
                 self._co._valid = False
@@ -103,10 +111,18 @@ class CommunicationHandle:
         self.is_ready()
 
     def schedule_wait(self, stream=None):
-        """Make `stream` wait for the exchange without blocking the host
-        (communication_handle::schedule_wait, :832-856)."""
-        if self._event is not None and stream is not None:
-            stream.wait_event(self._event)
+        """Make `stream` (None = the current stream) wait for the exchange without blocking the
+        host (communication_handle::schedule_wait, communication_object.hpp:832-856, 918-945).
+        Afterwards co.has_scheduled_exchange() is True until wait() or the next exchange."""
+        import torch
+        if self._event is None or self._co is None:
+            return
+        stream = stream if stream is not None else torch.cuda.current_stream(self._stream.device)
+        stream.wait_event(self._event)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self._co._scheduled_event = ev
+        self._co._valid = False  # a new exchange may start; it completes this one first
 
 
 class CommunicationObject:
@@ -122,6 +138,7 @@ class CommunicationObject:
         self._bufs = {}
         self._host = {}
         self._valid = False
+        self._scheduled_event = None
         self._host_group = None
         if staging == "host" and context.distributed is not None and context.size() > 1:
             dist = context.distributed
@@ -199,11 +216,44 @@ class CommunicationObject:
         return b
 
     # -- exchange ------------------------------------------------------------------------------
+    def has_scheduled_exchange(self) -> bool:
+        """A schedule_wait()-ed exchange whose completion has not been awaited on the host."""
+        return self._scheduled_event is not None
+
+    def complete_schedule_exchange(self):
+        """communication_object::complete_schedule_exchange (:950-968)."""
+        ev, self._scheduled_event = self._scheduled_event, None
+        if ev is not None:
+            ev.synchronize()
+            self._valid = False
+
+    @staticmethod
+    def _as_list(buffer_infos):
+        if len(buffer_infos) == 1 and isinstance(buffer_infos[0], (list, tuple)):
+            return list(buffer_infos[0])
+        return list(buffer_infos)
+
     def exchange(self, *buffer_infos) -> CommunicationHandle:
+        """Non-blocking exchange on the current stream (communication_object::exchange,
+        :271-285): pack, transport, unpack are stream-ordered; wait() blocks the host."""
         import torch
-        bis = list(buffer_infos[0]) if (len(buffer_infos) == 1 and
-                                         isinstance(buffer_infos[0], (list, tuple))) \
-            else list(buffer_infos)
+        bis = self._as_list(buffer_infos)
+        stream = torch.cuda.current_stream(bis[0].field.device) if bis else None
+        return self._start(bis, stream)
+
+    def schedule_exchange(self, stream, *buffer_infos) -> CommunicationHandle:
+        """communication_object::schedule_exchange (:287-330): the exchange starts after all
+        work submitted to `stream` (None = the current stream) so far, without blocking the
+        host; call schedule_wait(stream) on the handle to order later work after the unpack."""
+        import torch
+        bis = self._as_list(buffer_infos)
+        if stream is None and bis:
+            stream = torch.cuda.current_stream(bis[0].field.device)
+        return self._start(bis, stream)
+
+    def _start(self, bis, stream) -> CommunicationHandle:
+        import torch
+        self.complete_schedule_exchange()
         if self._valid:
             raise RuntimeError("earlier exchange operation was not finished")
         if not bis:
@@ -211,34 +261,32 @@ class CommunicationObject:
         device = bis[0].field.device
         plan = self.plan(bis)
         send, recv = self.buffers(plan, device)
-        stream = torch.cuda.current_stream(device)
         fptrs = _ghx.ptr_array([bi.field.data_ptr() for bi in bis])
         sptrs = _ghx.ptr_array([t.data_ptr() for t in send])
         rptrs = _ghx.ptr_array([t.data_ptr() for t in recv])
         self._valid = True
-        if self.fuse_self and self.all_self(plan):
-            # every message stays on this device: pack + unpack in one launch
-            _ghx.call("ghx_exchange_self", plan.h, fptrs, len(bis), sptrs, len(send),
-                      stream.cuda_stream)
+        with torch.cuda.stream(stream):
+            if self.fuse_self and self.all_self(plan):
+                # every message stays on this device: pack + unpack in one launch
+                _ghx.call("ghx_exchange_self", plan.h, fptrs, len(bis), sptrs, len(send),
+                          stream.cuda_stream)
+            else:
+                _ghx.call("ghx_exchange_pack", plan.h, fptrs, len(bis), sptrs, len(send),
+                          stream.cuda_stream)
+                me = self.context.rank()
+                sends = [(x["rank"], x["tag"], send[i][:x["size"]])
+                         for i, x in enumerate(plan.send) if x["rank"] != me]
+                recvs = [(x["rank"], x["tag"], recv[i][:x["size"]])
+                         for i, x in enumerate(plan.recv) if x["rank"] != me]
+                if self.staging == "host":
+                    self._exchange_host_staged(plan, sends, recvs, stream)
+                else:
+                    for w in route(self.context, sends, recvs):
+                        w.wait()  # NCCL: the stream waits for the recvs, the host does not
+                _ghx.call("ghx_exchange_unpack", plan.h, fptrs, len(bis), rptrs, len(recv),
+                          stream.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(stream)
-            return CommunicationHandle(self, stream, ev)
-        _ghx.call("ghx_exchange_pack", plan.h, fptrs, len(bis), sptrs, len(send),
-                  stream.cuda_stream)
-        me = self.context.rank()
-        sends = [(x["rank"], x["tag"], send[i][:x["size"]]) for i, x in enumerate(plan.send)
-                 if x["rank"] != me]
-        recvs = [(x["rank"], x["tag"], recv[i][:x["size"]]) for i, x in enumerate(plan.recv)
-                 if x["rank"] != me]
-        if self.staging == "host":
-            self._exchange_host_staged(plan, sends, recvs, stream)
-        else:
-            for w in route(self.context, sends, recvs):
-                w.wait()  # stream-ordered for NCCL: the unpack below is queued behind the recvs
-        _ghx.call("ghx_exchange_unpack", plan.h, fptrs, len(bis), rptrs, len(recv),
-                  stream.cuda_stream)
-        ev = torch.cuda.Event()
-        ev.record(stream)
         return CommunicationHandle(self, stream, ev)
 
     def _host_buffers(self, plan, sends, recvs):

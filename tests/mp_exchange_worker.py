@@ -8,7 +8,7 @@ With mode "bulk" the exchange is the zero-copy BulkCommunicationObject instead: 
 its send regions straight into the peers' fields through IPC mappings (same GPU here, peer
 GPUs over xGMI on a multi-GPU node).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk]"""
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk|sched]"""
 import os
 import sys
 
@@ -48,6 +48,14 @@ def main():
             co.add_field(pc(fd))
             for _ in range(reps):
                 co.exchange().wait()
+        elif mode == "sched":  # schedule_exchange on a side stream, host-staged transport
+            co = R.make_communication_object(ctx, staging="host")
+            s = torch.cuda.Stream()
+            for _ in range(reps):
+                h = co.schedule_exchange(s, [pc(fd)])
+                h.schedule_wait(s)
+                assert co.has_scheduled_exchange()
+                h.wait()
         else:
             co = R.make_communication_object(ctx, staging="host")
             for _ in range(reps):

@@ -27,7 +27,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("mode", ["staged", "bulk"])
+@pytest.mark.parametrize("mode", ["staged", "bulk", "sched"])
 @pytest.mark.parametrize("parts,N,Hw", [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)])
 def test_exchange_multi_process(parts, N, Hw, mode):
     """staged: CommunicationObject(staging="host") over gloo; bulk: zero-copy IPC puts."""
