@@ -197,6 +197,9 @@ struct exchange_plan
     std::vector<xbuffer> send, recv;
     std::unique_ptr<splan> spack, sunpack;
     std::unique_ptr<uplan> upack, uunpack;
+    // the fused self exchange's own pack/unpack plans when its tile size differs from the
+    // two-launch path's (g_tune.self_tile_bytes); null = use spack/sunpack
+    std::unique_ptr<splan> self_pack, self_unpack;
     int32_t n_items = 0;
     mutable int self_ok = -1;  // lazily checked: may pack and unpack be fused (all self)?
 
@@ -209,17 +212,23 @@ struct exchange_plan
         for (size_t i = 0; ok && i < send.size(); ++i)
             ok = send[i].first_id == recv[i].first_id && send[i].second_id == recv[i].second_id &&
                  send[i].size == recv[i].size;
-        if (ok) ok = spack->host_segs.size() == sunpack->host_segs.size() &&
-                     spack->n_tiles == sunpack->n_tiles;
-        for (size_t k = 0; ok && k < spack->host_segs.size(); ++k)
+        if (ok) ok = same_tiling(*spack, *sunpack);
+        self_ok = ok ? 1 : 0;
+        return ok;
+    }
+
+    // pack segment k and unpack segment k cover the same buffer bytes with the same tiling
+    static bool same_tiling(const splan& p, const splan& q)
+    {
+        bool ok = p.host_segs.size() == q.host_segs.size() && p.n_tiles == q.n_tiles;
+        for (size_t k = 0; ok && k < p.host_segs.size(); ++k)
         {
-            const auto& a = spack->host_segs[k];
-            const auto& b = sunpack->host_segs[k];
+            const auto& a = p.host_segs[k];
+            const auto& b = q.host_segs[k];
             ok = a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
                  a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes && a.partner < 0 &&
                  b.partner < 0;
         }
-        self_ok = ok ? 1 : 0;
         return ok;
     }
 };
@@ -410,6 +419,17 @@ int ghx_tune(const char* key, int32_t value)
         {
             if (value < 0 || value > 1) throw invalid("pair must be 0 or 1");
             g_tune.pair = value;
+        }
+        else if (k == "self_tile_bytes")
+        {
+            if (value < 1024 || uint32_t(value) > kMaxTileBytes || (value & (value - 1)))
+                throw invalid("self_tile_bytes must be a power of two in [1 KiB, 1 MiB]");
+            g_tune.self_tile_bytes = uint32_t(value);
+        }
+        else if (k == "xcd_pair")
+        {
+            if (value < 0 || value > 1) throw invalid("xcd_pair must be 0 or 1");
+            g_tune.xcd_pair = value;
         }
         else if (k == "u_tile_rows")
         {
@@ -815,9 +835,32 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
             if (!sent.empty())
                 (receive ? ex->sunpack : ex->spack) =
                     std::make_unique<splan>(sent.data(), int(sent.size()), receive ? 1 : 0);
+            if (!sent.empty() && g_tune.self_tile_bytes != g_tune.tile_bytes)
+            {
+                // candidate plans for the fused self exchange (kept only if it is fusable)
+                const uint32_t saved = g_tune.tile_bytes;
+                g_tune.tile_bytes = g_tune.self_tile_bytes;
+                try
+                {
+                    (receive ? ex->self_unpack : ex->self_pack) =
+                        std::make_unique<splan>(sent.data(), int(sent.size()), receive ? 1 : 0);
+                }
+                catch (...)
+                {
+                    g_tune.tile_bytes = saved;
+                    throw;
+                }
+                g_tune.tile_bytes = saved;
+            }
             if (!uent.empty())
                 (receive ? ex->uunpack : ex->upack) =
                     std::make_unique<uplan>(uent.data(), int(uent.size()), receive ? 1 : 0);
+        }
+        if (!ex->self_fusable() || !ex->self_pack || !ex->self_unpack ||
+            !exchange_plan::same_tiling(*ex->self_pack, *ex->self_unpack))
+        {
+            ex->self_pack.reset();
+            ex->self_unpack.reset();
         }
         *out = ex.release();
         return GHX_OK;
@@ -905,13 +948,14 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
         check_ptr(ex, "exchange");
         if (!ex->self_fusable())
             throw invalid("exchange is not an all-self exchange with matching segments");
-        const splan& p = *ex->spack;
+        const splan& p = ex->self_pack ? *ex->self_pack : *ex->spack;
+        const splan& q = ex->self_unpack ? *ex->self_unpack : *ex->sunpack;
         if (n_fields <= p.max_field_slot || n_buffers <= p.max_buf_slot)
             throw invalid("pointer arrays do not cover the plan's slots");
-        if (!p.dev.segs || !ex->sunpack->dev.segs) throw hip_error("plan has no device tables");
+        if (!p.dev.segs || !q.dev.segs) throw hip_error("plan has no device tables");
         kargs a{};
         a.segs = p.dev.segs;
-        a.segs2 = ex->sunpack->dev.segs;
+        a.segs2 = q.dev.segs;
         a.tile_seg = p.dev.tiles;
         a.n_tiles = p.n_tiles;
         for (int i = 0; i <= p.max_field_slot; ++i)

@@ -30,6 +30,9 @@ struct tuning
     int nt = 0;                     // 0 default, 1 nt stores, 2 nt loads + stores, 3 nt loads
     int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
     uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
+    uint32_t self_tile_bytes = 4096;   // the same for the fused self exchange (k_self: each
+                                       // tile is packed, then unpacked by one workgroup;
+                                       // measured best 4 KiB vs 8 KiB for two launches)
     uint32_t small_tile_rows = 4096;   // rows per tile of segments with short rows
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
@@ -46,6 +49,10 @@ struct tuning
     int short_pol = 0;                 // field-side cache policy of short-row segments:
                                        // bit 0 non-temporal loads (pack), bit 1 sc1 stores
                                        // (unpack)
+    int xcd_pair = 1;                  // dispatch the tiles of line-sharing short-row segment
+                                       // pairs in lock-step groups of 8, so tile t of both
+                                       // halves lands on the same XCD (blocks are dealt
+                                       // round-robin over the 8 XCDs) at the same time
 };
 extern tuning g_tune;
 

@@ -23,6 +23,43 @@ int wlog2_of(uint64_t v)  // log2 of the largest power of two <= 16 dividing v
 
 uint32_t tiles_of(uint32_t bytes, uint32_t tb) { return (bytes + tb - 1) / tb; }
 
+// Short-row segments of one field whose rows interleave in memory: row r of `a` and row r-1 of
+// `b` share a 128-B line (0 < a.field_off + a.stride[0] - b.field_off < 128, the pieces disjoint).
+// For a unit-stride field these are the two x-normal faces (and x-edges) of a halo: the -x piece
+// of row y+1 sits right after the +x piece of row y. Returns partner[i] (or -1), symmetric.
+std::vector<int32_t> line_partners(const std::vector<seg_s>& segs)
+{
+    std::vector<int32_t> partner(segs.size(), -1);
+    for (size_t i = 0; i < segs.size(); ++i)
+    {
+        const auto& a = segs[i];
+        if (partner[i] >= 0 || a.partner >= 0 || a.row_bytes >= g_tune.small_row_bytes ||
+            a.n_outer < 1 || a.bytes / a.row_bytes < 2)
+            continue;
+        for (size_t j = 0; j < segs.size(); ++j)
+        {
+            if (j == i || partner[j] >= 0 || segs[j].partner >= 0) continue;
+            const auto& b = segs[j];
+            bool same = b.field_slot == a.field_slot && b.row_bytes == a.row_bytes &&
+                        b.n_outer == a.n_outer && b.bytes == a.bytes;
+            for (int k = 0; same && k < 4; ++k)
+                same = b.ext[k] == a.ext[k] && b.stride[k] == a.stride[k];
+            if (!same) continue;
+            const int64_t d = a.field_off + a.stride[0] - b.field_off;
+            if (d <= 0 || d >= 128 || d < int64_t(a.row_bytes)) continue;
+            partner[i] = int32_t(j);
+            partner[j] = int32_t(i);
+            break;
+        }
+    }
+    return partner;
+}
+
+std::vector<int32_t> line_partners(const std::vector<seg_u>& segs)
+{
+    return std::vector<int32_t>(segs.size(), -1);
+}
+
 // Tile table: per tile {segment, tile index within the segment}. Segments with short rows
 // (request-bound: one memory request per row) may use a different tile size from streaming
 // segments; the dispatch order of tiles is a tuning knob (hardware dispatches in blockIdx order).
@@ -74,8 +111,38 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
                 return (segs[a].row_bytes < g_tune.small_row_bytes) >
                        (segs[b].row_bytes < g_tune.small_row_bytes);
             });
+        std::vector<int32_t> partner(segs.size(), -1);
+        if (g_tune.order == 1 && g_tune.xcd_pair && !g_tune.pair) partner = line_partners(segs);
+        // Line-sharing pairs first, in lock-step groups of 8 tiles: tile t of one half at block
+        // 16k + i, tile t of the other at 16k + 8 + i -> the same XCD (blocks are dealt
+        // round-robin over the 8 XCDs) at about the same time, so each shared line is fetched
+        // once into that XCD's L2 and both halves' partial writes merge there. A short group is
+        // padded with tiles of the other segments so the alignment holds.
+        std::vector<std::pair<uint32_t, uint32_t>> rest;
         for (uint32_t i : idx)
-            for (uint32_t t : per[i]) emit(i, t);
+            if (partner[i] < 0)
+                for (uint32_t t : per[i]) rest.emplace_back(i, t);
+        size_t next = 0;
+        for (uint32_t i : idx)
+        {
+            const int32_t j = partner[i];
+            if (j < 0 || uint32_t(j) < i || per[i].size() != per[size_t(j)].size())
+            {
+                if (j >= 0 && per[i].size() != per[size_t(j)].size())
+                    for (uint32_t t : per[i]) emit(i, t);  // (cannot happen: equal bytes)
+                continue;
+            }
+            const size_t n = per[i].size();
+            for (size_t k = 0; k < n; k += 8)
+            {
+                const size_t m = std::min<size_t>(8, n - k);
+                for (size_t u = 0; u < m; ++u) emit(uint32_t(j), per[size_t(j)][k + u]);
+                for (size_t u = m; u < 8 && next < rest.size(); ++u, ++next)
+                    emit(rest[next].first, rest[next].second);
+                for (size_t u = 0; u < m; ++u) emit(i, per[i][k + u]);
+            }
+        }
+        for (; next < rest.size(); ++next) emit(rest[next].first, rest[next].second);
     }
     return out;
 }

@@ -11,8 +11,6 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULTS = dict(unroll=4, nt=0, grid_cap=0, tile_bytes=16384, small_tile_rows=4096,
-                small_row_bytes=64, order=1)
 
 
 def main():
@@ -40,9 +38,8 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     out = []
     for cfg in configs:
-        knobs = dict(DEFAULTS)
-        knobs.update(cfg)
-        for k, v in knobs.items():
+        _ghx.call("ghx_tune", b"reset", 0)
+        for k, v in cfg.items():
             _ghx.call("ghx_tune", k.encode(), int(v))
         co = R.make_communication_object(ctx)
         bis = [pc(fd)]
