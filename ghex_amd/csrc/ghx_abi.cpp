@@ -426,6 +426,11 @@ int ghx_tune(const char* key, int32_t value)
                 throw invalid("self_tile_bytes must be a power of two in [1 KiB, 1 MiB]");
             g_tune.self_tile_bytes = uint32_t(value);
         }
+        else if (k == "self_chunk")
+        {
+            if (value < 0 || (value & 15)) throw invalid("self_chunk must be a multiple of 16 (0: tile)");
+            g_tune.self_chunk = uint32_t(value);
+        }
         else if (k == "xcd_pair")
         {
             if (value < 0 || value > 1) throw invalid("xcd_pair must be 0 or 1");
@@ -956,6 +961,7 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
         kargs a{};
         a.segs = p.dev.segs;
         a.segs2 = q.dev.segs;
+        a.chunk = g_tune.self_chunk;
         a.tile_seg = p.dev.tiles;
         a.n_tiles = p.n_tiles;
         for (int i = 0; i <= p.max_field_slot; ++i)

@@ -49,6 +49,9 @@ struct tuning
     int short_pol = 0;                 // field-side cache policy of short-row segments:
                                        // bit 0 non-temporal loads (pack), bit 1 sc1 stores
                                        // (unpack)
+    uint32_t self_chunk = 0;           // fused self exchange: a workgroup packs, then unpacks,
+                                       // this many buffer bytes at a time (0: the whole tile;
+                                       // 4-32 KiB chunks measured no faster, 4 KiB slower)
     int xcd_pair = 1;                  // dispatch the tiles of line-sharing short-row segment
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt
@@ -136,7 +139,7 @@ struct kargs
     const void* segs2;         // fused self exchange: the unpack segments (1:1 with segs)
     const uint32_t* tile_seg;  // per tile: {segment index, tile index within the segment}
     uint32_t n_tiles;
-    uint32_t pad0;
+    uint32_t chunk;            // fused self exchange: pack/unpack alternate per chunk (0: tile)
     uint64_t field_ptr[GHX_MAX_SLOTS];
     uint64_t buf_ptr[GHX_MAX_SLOTS];
 };

@@ -423,10 +423,17 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
         wp = min(wp, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
         int wu = min(int(q.wlog2), ptr_wlog2(reinterpret_cast<uint64_t>(field_u)));
         wu = min(wu, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
-        copy_any<true, U, NT>(s, field_p, buf, start, end, wp);
-        __syncthreads();  // workgroup release/acquire: the tile's buffer bytes are complete
-        copy_any<false, U, NT>(q, field_u, buf, start, end, wu);
-        __syncthreads();  // keep tiles of a grid-stride loop ordered for the next iteration
+        // Whole tile, or in chunks of a.chunk buffer bytes (g_tune.self_chunk, a knob: keeping
+        // the re-read bytes in L2 this way measured no faster).
+        const uint32_t chunk = a.chunk ? a.chunk : s.tile_bytes;
+        for (uint32_t c = start; c < end; c += chunk)
+        {
+            const uint32_t ce = min(c + chunk, end);
+            copy_any<true, U, NT>(s, field_p, buf, c, ce, wp);
+            __syncthreads();  // workgroup release/acquire: the chunk's buffer bytes are complete
+            copy_any<false, U, NT>(q, field_u, buf, c, ce, wu);
+            __syncthreads();  // the next chunk / tile reuses the lanes
+        }
     }
 }
 
