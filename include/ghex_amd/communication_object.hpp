@@ -1,0 +1,606 @@
+// ghex_amd/communication_object.hpp — the reference's host-side exchange API in C++ over the C
+// ABI of libghx.so: context, domain descriptors, halo generators, make_pattern, pattern(field)
+// -> buffer_info, make_communication_object, exchange(...) -> handle.wait().
+//
+// Mirrors (paths relative to the GHEX v0.8.0 tree):
+//   ghex::context                                    include/ghex/context.hpp
+//   structured::regular::{domain_descriptor, halo_generator}
+//                                                    include/ghex/structured/regular/{domain_descriptor,halo_generator}.hpp
+//   unstructured::{domain_descriptor, halo_generator} include/ghex/unstructured/user_concepts.hpp:37-256
+//   make_pattern<grid>(ctx, halo_gen, domains)       include/ghex/pattern_container.hpp:112-120
+//   pattern_container::operator()(field) -> buffer_info   pattern_container.hpp:88-95, buffer_info.hpp
+//   communication_object::exchange / schedule_exchange, communication_handle::wait / is_ready /
+//   schedule_wait                                    include/ghex/communication_object.hpp:78-130, 271-330, 801-968
+//
+// What an exchange does (the reference's stream-aware branch, communication_object.hpp:703-767):
+//   plan once per set of fields (ghx_exchange_create = communication_object::allocate: one buffer
+//   per domain pair, fields in argument order with alignof padding, tags = pattern tag + a
+//   per-container offset); then per exchange, on the object's stream:
+//     all messages self messages -> ONE fused pack+unpack launch (ghx_exchange_self);
+//     otherwise -> ONE pack launch for every send buffer (ghx_exchange_pack), one transport group
+//     of the peer messages (rccl_transport: ncclSend/ncclRecv over xGMI), ONE unpack launch for
+//     every receive buffer (ghx_exchange_unpack). Self messages never leave the device: their
+//     receive buffer IS the send buffer.
+// The host never blocks inside exchange(); handle.wait() synchronises with the stream.
+// Errors throw std::runtime_error (the reference's convention). Link with -lghx (+ -lrccl for
+// rccl_transport).
+#pragma once
+
+#include <ghx.h>
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <type_traits>
+#include <vector>
+
+#include "transport.hpp"
+
+namespace ghex_amd
+{
+inline void check_ghx(int rc, const char* what)
+{
+    if (rc != GHX_OK) throw std::runtime_error(std::string(what) + " failed: " + ghx_last_error());
+}
+
+// ghex::context (include/ghex/context.hpp): the process group the patterns and exchanges span.
+class context
+{
+    transport* m_transport;
+
+  public:
+    explicit context(transport& t)
+    : m_transport{&t}
+    {
+    }
+    int rank() const { return m_transport->rank(); }
+    int size() const { return m_transport->size(); }
+    transport& get_transport() const { return *m_transport; }
+};
+
+namespace detail
+{
+template<typename T>
+void put(std::vector<char>& out, const T& v)
+{
+    const char* p = reinterpret_cast<const char*>(&v);
+    out.insert(out.end(), p, p + sizeof(T));
+}
+template<typename T>
+T get(const std::vector<char>& in, std::size_t& pos)
+{
+    if (pos + sizeof(T) > in.size()) throw std::runtime_error("malformed all_gather payload");
+    T v;
+    std::memcpy(&v, in.data() + pos, sizeof(T));
+    pos += sizeof(T);
+    return v;
+}
+}  // namespace detail
+
+// A pattern container: the halo maps of this rank's domains (one pattern per local domain), owned
+// by libghx (ghx_pattern). pattern(field) selects the pattern of the field's domain.
+class pattern_container;
+
+template<typename Field>
+struct buffer_info
+{
+    const pattern_container* pattern;
+    int local_index;
+    Field* field;
+};
+
+class pattern_container
+{
+    std::shared_ptr<ghx_pattern> m_p;
+    std::vector<int> m_ids;
+    int m_max_tag = 0;
+
+  public:
+    explicit pattern_container(ghx_pattern* p)
+    : m_p{p, [](ghx_pattern* q) { ghx_pattern_destroy(q); }}
+    {
+        int32_t n = 0;
+        check_ghx(ghx_pattern_num_domains(p, &n), "ghx_pattern_num_domains");
+        for (int32_t i = 0; i < n; ++i)
+        {
+            int32_t id = 0;
+            check_ghx(ghx_pattern_domain_id(p, i, &id), "ghx_pattern_domain_id");
+            m_ids.push_back(id);
+        }
+        int32_t mt = 0;
+        check_ghx(ghx_pattern_max_tag(p, &mt), "ghx_pattern_max_tag");
+        m_max_tag = mt;
+    }
+    const ghx_pattern* handle() const { return m_p.get(); }
+    int max_tag() const { return m_max_tag; }  // pattern_container::max_tag (:78-83)
+    std::size_t size() const { return m_ids.size(); }
+
+    // pattern_container::operator()(field) (pattern_container.hpp:88-95)
+    template<typename Field>
+    buffer_info<Field> operator()(Field& field) const
+    {
+        for (std::size_t i = 0; i < m_ids.size(); ++i)
+            if (m_ids[i] == int(field.domain_id())) return {this, int(i), &field};
+        throw std::runtime_error("field's domain id is not a local domain of this pattern");
+    }
+};
+
+namespace structured
+{
+namespace regular
+{
+// structured::regular::domain_descriptor (3-D, int ids), inclusive first/last global coords.
+class domain_descriptor
+{
+    int m_id;
+    std::array<int, 3> m_first, m_last;
+
+  public:
+    domain_descriptor(int id, const std::array<int, 3>& first, const std::array<int, 3>& last)
+    : m_id{id}
+    , m_first{first}
+    , m_last{last}
+    {
+    }
+    int domain_id() const { return m_id; }
+    const std::array<int, 3>& first() const { return m_first; }
+    const std::array<int, 3>& last() const { return m_last; }
+};
+
+// structured::regular::halo_generator (halo_generator.hpp:61-90): global box, halos
+// (dim0-, dim0+, dim1-, dim1+, dim2-, dim2+), periodicity.
+struct halo_generator
+{
+    std::array<int, 3> global_first, global_last;
+    std::array<int, 6> halos;
+    std::array<bool, 3> periodic;
+};
+
+// make_pattern<structured::grid> (include/ghex/structured/pattern.hpp:214-571): the domains of
+// all ranks are all-gathered through the context's transport, libghx intersects.
+inline pattern_container make_pattern(context& ctx, const halo_generator& hg,
+                                      const std::vector<domain_descriptor>& domains)
+{
+    std::vector<char> mine;
+    detail::put(mine, std::int32_t(domains.size()));
+    for (const auto& d : domains)
+    {
+        detail::put(mine, std::int32_t(d.domain_id()));
+        for (int k = 0; k < 3; ++k) detail::put(mine, std::int32_t(d.first()[k]));
+        for (int k = 0; k < 3; ++k) detail::put(mine, std::int32_t(d.last()[k]));
+    }
+    const auto all = ctx.get_transport().all_gather(mine);
+    std::vector<ghx_regular_domain> doms;
+    for (std::size_t r = 0; r < all.size(); ++r)
+    {
+        std::size_t pos = 0;
+        const auto n = detail::get<std::int32_t>(all[r], pos);
+        for (std::int32_t i = 0; i < n; ++i)
+        {
+            ghx_regular_domain g{};
+            g.id = detail::get<std::int32_t>(all[r], pos);
+            g.rank = std::int32_t(r);
+            for (int k = 0; k < 3; ++k) g.first[k] = detail::get<std::int32_t>(all[r], pos);
+            for (int k = 0; k < 3; ++k) g.last[k] = detail::get<std::int32_t>(all[r], pos);
+            doms.push_back(g);
+        }
+    }
+    std::int32_t per[3];
+    for (int k = 0; k < 3; ++k) per[k] = hg.periodic[std::size_t(k)] ? 1 : 0;
+    ghx_pattern* p = nullptr;
+    check_ghx(ghx_regular_pattern_create(3, doms.data(), std::int32_t(doms.size()),
+                                         hg.global_first.data(), hg.global_last.data(),
+                                         hg.halos.data(), per, ctx.rank(), &p),
+              "ghx_regular_pattern_create");
+    return pattern_container(p);
+}
+}  // namespace regular
+}  // namespace structured
+
+namespace unstructured
+{
+// unstructured::domain_descriptor (user_concepts.hpp:143-175): all global ids in storage order
+// and the local ids of the outer (halo) cells.
+class domain_descriptor
+{
+    int m_id;
+    std::vector<std::int64_t> m_gids, m_outer;
+
+  public:
+    domain_descriptor(int id, std::vector<std::int64_t> gids, std::vector<std::int64_t> outer_lids)
+    : m_id{id}
+    , m_gids(std::move(gids))
+    , m_outer(std::move(outer_lids))
+    {
+    }
+    int domain_id() const { return m_id; }
+    std::size_t size() const { return m_gids.size(); }
+    const std::vector<std::int64_t>& gids() const { return m_gids; }
+    const std::vector<std::int64_t>& outer_lids() const { return m_outer; }
+};
+
+// unstructured::halo_generator (user_concepts.hpp:234-253): every outer gid (default) or an
+// explicit list of halo gids.
+struct halo_generator
+{
+    bool all_outer = true;
+    std::vector<std::int64_t> gids;
+};
+
+// make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370)
+inline pattern_container make_pattern(context& ctx, const halo_generator& hg,
+                                      const std::vector<domain_descriptor>& domains)
+{
+    std::vector<char> mine;
+    detail::put(mine, std::int32_t(domains.size()));
+    for (const auto& d : domains)
+    {
+        detail::put(mine, std::int32_t(d.domain_id()));
+        detail::put(mine, std::int64_t(d.gids().size()));
+        for (auto g : d.gids()) detail::put(mine, g);
+        detail::put(mine, std::int64_t(d.outer_lids().size()));
+        for (auto l : d.outer_lids()) detail::put(mine, l);
+        detail::put(mine, std::int64_t(hg.all_outer ? -1 : std::int64_t(hg.gids.size())));
+        if (!hg.all_outer)
+            for (auto g : hg.gids) detail::put(mine, g);
+    }
+    const auto all = ctx.get_transport().all_gather(mine);
+    std::vector<std::int32_t> ids, ranks;
+    std::vector<std::int64_t> gids, gc, outer, oc, hgid, hc;
+    for (std::size_t r = 0; r < all.size(); ++r)
+    {
+        std::size_t pos = 0;
+        const auto n = detail::get<std::int32_t>(all[r], pos);
+        for (std::int32_t i = 0; i < n; ++i)
+        {
+            ids.push_back(detail::get<std::int32_t>(all[r], pos));
+            ranks.push_back(std::int32_t(r));
+            const auto ng = detail::get<std::int64_t>(all[r], pos);
+            gc.push_back(ng);
+            for (std::int64_t k = 0; k < ng; ++k) gids.push_back(detail::get<std::int64_t>(all[r], pos));
+            const auto no = detail::get<std::int64_t>(all[r], pos);
+            oc.push_back(no);
+            for (std::int64_t k = 0; k < no; ++k) outer.push_back(detail::get<std::int64_t>(all[r], pos));
+            const auto nh = detail::get<std::int64_t>(all[r], pos);
+            hc.push_back(nh);
+            for (std::int64_t k = 0; k < nh; ++k) hgid.push_back(detail::get<std::int64_t>(all[r], pos));
+        }
+    }
+    ghx_pattern* p = nullptr;
+    check_ghx(ghx_unstructured_pattern_create(std::int32_t(ids.size()), ids.data(), ranks.data(),
+                                              gids.data(), gc.data(), outer.data(), oc.data(),
+                                              hgid.data(), hc.data(), ctx.rank(), &p),
+              "ghx_unstructured_pattern_create");
+    return pattern_container(p);
+}
+}  // namespace unstructured
+
+class communication_object;
+
+// communication_handle (communication_object.hpp:78-130)
+class communication_handle
+{
+    communication_object* m_co = nullptr;
+    hipEvent_t m_done = nullptr;
+
+  public:
+    communication_handle() = default;
+    communication_handle(communication_object* co, hipEvent_t done)
+    : m_co{co}
+    , m_done{done}
+    {
+    }
+    inline void wait();
+    inline bool is_ready();
+    void progress() { (void)is_ready(); }
+    // make `stream` wait for the exchange without blocking the host (:832-856, 918-945)
+    void schedule_wait(hipStream_t stream)
+    {
+        if (m_done) check_hip(hipStreamWaitEvent(stream, m_done, 0), "hipStreamWaitEvent");
+    }
+};
+
+struct communication_options
+{
+    bool fuse_self = true;                // all-self exchanges as one launch
+    bool self_through_transport = false;  // route self messages through the transport too
+                                          // (transport testing; oomph also sends to self)
+};
+
+// communication_object<grid, domain_id> (make_communication_object, :1105-1112)
+class communication_object
+{
+  public:
+    using options = communication_options;
+
+  private:
+    struct buf
+    {
+        std::int32_t first_id, second_id, rank, tag;
+        std::uint64_t size;
+        void* data = nullptr;
+        bool owned = true;
+    };
+    struct plan
+    {
+        ghx_exchange* ex = nullptr;
+        std::vector<buf> send, recv;
+        bool fused = false;
+        std::vector<void*> sptr, rptr;
+        ~plan()
+        {
+            for (auto* v : {&send, &recv})
+                for (auto& b : *v)
+                    if (b.owned && b.data) (void)hipFree(b.data);
+            if (ex) ghx_exchange_destroy(ex);
+        }
+    };
+
+    context* m_ctx;
+    options m_opt;
+    hipStream_t m_stream = nullptr;
+    hipEvent_t m_done = nullptr, m_start = nullptr;
+    bool m_valid = false;
+    std::map<std::string, std::unique_ptr<plan>> m_plans;
+
+  public:
+    explicit communication_object(context& ctx, options opt = {})
+    : m_ctx{&ctx}
+    , m_opt{opt}
+    {
+        // a non-blocking stream of the greatest priority, like the reference's device::stream
+        // (include/ghex/device/cuda/stream.hpp:30-37)
+        int lo = 0, hi = 0;
+        check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+        check_hip(hipStreamCreateWithPriority(&m_stream, hipStreamNonBlocking, hi), "hipStreamCreate");
+        check_hip(hipEventCreateWithFlags(&m_done, hipEventDisableTiming), "hipEventCreate");
+        check_hip(hipEventCreateWithFlags(&m_start, hipEventDisableTiming), "hipEventCreate");
+    }
+    communication_object(const communication_object&) = delete;
+    communication_object& operator=(const communication_object&) = delete;
+    ~communication_object()
+    {
+        if (m_stream) (void)hipStreamSynchronize(m_stream);
+        m_plans.clear();
+        if (m_done) (void)hipEventDestroy(m_done);
+        if (m_start) (void)hipEventDestroy(m_start);
+        if (m_stream) (void)hipStreamDestroy(m_stream);
+    }
+
+    hipStream_t stream() const { return m_stream; }
+
+    // exchange(pattern(f1), pattern(f2), ...) (:271-285)
+    template<typename... Fields>
+    communication_handle exchange(buffer_info<Fields>... bis)
+    {
+        return start(nullptr, {item_of(bis)...}, {ptr_of(bis)...});
+    }
+    // exchange(first, last) over buffer_infos of one field type (:349-355)
+    template<typename Iterator>
+    communication_handle exchange(Iterator first, Iterator last)
+    {
+        std::vector<ghx_exchange_item> items;
+        std::vector<void*> ptrs;
+        for (auto it = first; it != last; ++it)
+        {
+            items.push_back(item_of(*it));
+            ptrs.push_back(ptr_of(*it));
+        }
+        return start(nullptr, std::move(items), std::move(ptrs));
+    }
+    // schedule_exchange(stream, ...) (:287-330): starts after the work already on `stream`,
+    // never blocks the host; pair with handle.schedule_wait(stream).
+    template<typename... Fields>
+    communication_handle schedule_exchange(hipStream_t stream, buffer_info<Fields>... bis)
+    {
+        return start(stream, {item_of(bis)...}, {ptr_of(bis)...});
+    }
+
+    // plan facts (tests / benchmarks)
+    std::size_t num_plans() const { return m_plans.size(); }
+
+  private:
+    friend class communication_handle;
+    void finish()
+    {
+        check_hip(hipEventSynchronize(m_done), "hipEventSynchronize");
+        m_valid = false;
+    }
+    bool ready()
+    {
+        const hipError_t e = hipEventQuery(m_done);
+        if (e == hipErrorNotReady) return false;
+        check_hip(e, "hipEventQuery");
+        m_valid = false;
+        return true;
+    }
+
+    // tag offsets per distinct pattern container in argument order (:540-549) are assigned in
+    // start(); here only the per-field description
+    template<typename Field>
+    static ghx_exchange_item item_of(const buffer_info<Field>& bi)
+    {
+        ghx_exchange_item it;
+        std::memset(&it, 0, sizeof(it));
+        it.pattern = bi.pattern->handle();
+        it.local_index = bi.local_index;
+        describe(it, bi.field->desc());
+        it.align = std::int32_t(alignof(typename Field::value_type));
+        it.tag_offset = 0;
+        return it;
+    }
+    static void describe(ghx_exchange_item& it, const ghx_field_desc& d)
+    {
+        it.kind = 0;
+        it.field = d;
+    }
+    static void describe(ghx_exchange_item& it, const ghx_udata_desc& d)
+    {
+        it.kind = 1;
+        it.udata = d;
+    }
+    template<typename Field>
+    static void* ptr_of(const buffer_info<Field>& bi)
+    {
+        return const_cast<void*>(static_cast<const void*>(bi.field->data()));
+    }
+
+    // plan cache key: every member of every item (no padding bytes)
+    static std::string key_of(const std::vector<ghx_exchange_item>& items)
+    {
+        std::vector<char> k;
+        for (const auto& it : items)
+        {
+            detail::put(k, it.pattern);
+            detail::put(k, it.local_index);
+            detail::put(k, it.kind);
+            detail::put(k, it.align);
+            detail::put(k, it.tag_offset);
+            if (it.kind == 0)
+            {
+                const auto& f = it.field;
+                detail::put(k, f.dim);
+                detail::put(k, f.elem_size);
+                detail::put(k, f.num_components);
+                detail::put(k, f.has_components);
+                for (int d = 0; d < GHX_MAX_DIM; ++d)
+                {
+                    detail::put(k, f.layout[d]);
+                    detail::put(k, f.byte_strides[d]);
+                    detail::put(k, f.offsets[d]);
+                    detail::put(k, f.extents[d]);
+                }
+            }
+            else
+            {
+                const auto& u = it.udata;
+                detail::put(k, u.elem_size);
+                detail::put(k, u.levels);
+                detail::put(k, u.levels_first);
+                detail::put(k, u.index_stride);
+                detail::put(k, u.level_stride);
+            }
+        }
+        return std::string(k.begin(), k.end());
+    }
+
+    plan& plan_for(std::vector<ghx_exchange_item>& items)
+    {
+        std::map<const ghx_pattern*, std::int32_t> offsets;
+        std::int32_t acc = 0;
+        for (auto& it : items)
+        {
+            auto f = offsets.find(it.pattern);
+            if (f == offsets.end())
+            {
+                std::int32_t mt = 0;
+                check_ghx(ghx_pattern_max_tag(it.pattern, &mt), "ghx_pattern_max_tag");
+                f = offsets.emplace(it.pattern, acc).first;
+                acc += mt + 1;
+            }
+            it.tag_offset = f->second;
+        }
+        const std::string key = key_of(items);
+        auto found = m_plans.find(key);
+        if (found != m_plans.end()) return *found->second;
+        auto p = std::make_unique<plan>();
+        check_ghx(ghx_exchange_create(items.data(), std::int32_t(items.size()), &p->ex), "ghx_exchange_create");
+        const int me = m_ctx->rank();
+        for (int dir = 0; dir < 2; ++dir)
+        {
+            std::int32_t n = 0;
+            check_ghx(ghx_exchange_num_buffers(p->ex, dir, &n), "ghx_exchange_num_buffers");
+            auto& v = dir == 0 ? p->send : p->recv;
+            for (std::int32_t i = 0; i < n; ++i)
+            {
+                buf b{};
+                check_ghx(ghx_exchange_buffer(p->ex, dir, i, &b.first_id, &b.second_id, &b.rank, &b.tag, &b.size),
+                          "ghx_exchange_buffer");
+                v.push_back(b);
+            }
+        }
+        for (auto& b : p->send)
+            check_hip(hipMalloc(&b.data, std::max<std::uint64_t>(1, b.size)), "hipMalloc(send buffer)");
+        for (auto& b : p->recv)
+        {
+            if (b.rank == me && !m_opt.self_through_transport)
+            {
+                // self message: unpack straight from the matching send buffer
+                for (auto& s : p->send)
+                    if (s.first_id == b.first_id && s.second_id == b.second_id && s.rank == me)
+                    {
+                        b.data = s.data;
+                        b.owned = false;
+                    }
+            }
+            if (!b.data) check_hip(hipMalloc(&b.data, std::max<std::uint64_t>(1, b.size)), "hipMalloc(recv buffer)");
+        }
+        bool all_self = !m_opt.self_through_transport;
+        for (auto* v : {&p->send, &p->recv})
+            for (auto& b : *v) all_self = all_self && b.rank == me;
+        std::int32_t fusable = 0;
+        check_ghx(ghx_exchange_self_fusable(p->ex, &fusable), "ghx_exchange_self_fusable");
+        p->fused = m_opt.fuse_self && all_self && fusable;
+        for (auto& b : p->send) p->sptr.push_back(b.data);
+        for (auto& b : p->recv) p->rptr.push_back(b.data);
+        auto& ref = *p;
+        m_plans.emplace(std::move(key), std::move(p));
+        return ref;
+    }
+
+    communication_handle start(hipStream_t after, std::vector<ghx_exchange_item> items,
+                               std::vector<void*> fptrs)
+    {
+        if (m_valid) throw std::runtime_error("earlier exchange operation was not finished");
+        if (items.empty()) return {};
+        plan& p = plan_for(items);
+        if (after)
+        {
+            check_hip(hipEventRecord(m_start, after), "hipEventRecord");
+            check_hip(hipStreamWaitEvent(m_stream, m_start, 0), "hipStreamWaitEvent");
+        }
+        const auto nf = std::int32_t(fptrs.size());
+        const auto ns = std::int32_t(p.sptr.size()), nr = std::int32_t(p.rptr.size());
+        if (p.fused)
+            check_ghx(ghx_exchange_self(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream), "ghx_exchange_self");
+        else
+        {
+            check_ghx(ghx_exchange_pack(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream), "ghx_exchange_pack");
+            const int me = m_ctx->rank();
+            std::vector<message> sends, recvs;
+            for (auto& b : p.send)
+                if (b.rank != me || m_opt.self_through_transport) sends.push_back({b.data, b.size, b.rank, b.tag});
+            for (auto& b : p.recv)
+                if (b.rank != me || m_opt.self_through_transport) recvs.push_back({b.data, b.size, b.rank, b.tag});
+            if (!sends.empty() || !recvs.empty()) m_ctx->get_transport().exchange(sends, recvs, m_stream);
+            check_ghx(ghx_exchange_unpack(p.ex, fptrs.data(), nf, p.rptr.data(), nr, m_stream), "ghx_exchange_unpack");
+        }
+        check_hip(hipEventRecord(m_done, m_stream), "hipEventRecord");
+        m_valid = true;
+        return {this, m_done};
+    }
+};
+
+inline void communication_handle::wait()
+{
+    if (m_co) m_co->finish();
+    m_co = nullptr;
+}
+
+inline bool communication_handle::is_ready()
+{
+    if (!m_co) return true;
+    if (!m_co->ready()) return false;
+    m_co = nullptr;
+    return true;
+}
+
+inline communication_object make_communication_object(context& ctx)
+{
+    return communication_object(ctx);
+}
+}  // namespace ghex_amd

@@ -1,0 +1,287 @@
+// co_demo.cpp — drives the C++ communication object (include/ghex_amd/communication_object.hpp)
+// the way a GHEX application drives ghex::communication_object, and checks every cell.
+//
+//   co_demo loopback PX PY PZ N H       PX*PY*PZ ranks as threads on device 0 (loopback
+//                                        transport), one N^3 domain each of a periodic global
+//                                        grid, two fields (double, float) in ONE exchange; every
+//                                        cell of every rank vs the wrapped global index; twice
+//                                        (the second exchange reuses the cached plan/buffers)
+//   co_demo rccl N H SELF                one rank, RCCL communicator on device 0; SELF=1 sends the
+//                                        self messages through ncclSend/ncclRecv (group), SELF=0
+//                                        takes the fused self path
+//   co_demo unstructured FILE LEVELS     ranks as threads, domains from FILE (per line:
+//                                        "id n_gids gids... n_outer lids..."), one domain per rank;
+//                                        value(lid, level) = dom*10000 + gid*100 + level
+//                                        (test/unstructured/unstructured_test_case.hpp:345-388);
+//                                        every halo value vs its owner's encoding
+//   co_demo bench N H ITERS              one rank, host-inclusive microseconds per exchange
+//                                        (exchange + wait) on the fused self path
+// Prints one JSON line per rank / result; exit status 0 iff every cell matched.
+#include <ghex_amd/communication_object.hpp>
+#include <ghex_amd/data_descriptor.hpp>
+#include <ghex_amd/field_descriptor.hpp>
+#include <ghex_amd/rccl_transport.hpp>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <set>
+#include <sstream>
+#include <thread>
+
+using namespace ghex_amd;
+namespace R = ghex_amd::structured::regular;
+
+namespace
+{
+struct cube
+{
+    int N, H, E;
+    std::array<int, 3> parts, G, c;
+    long idx(int x, int y, int z) const { return (long(z) * E + y) * E + x; }
+    double expect(int x, int y, int z) const  // wrapped global linear index of local (x,y,z)
+    {
+        const int l[3] = {x, y, z};
+        long g[3];
+        for (int d = 0; d < 3; ++d) g[d] = ((long(c[d]) * N + l[d] - H) % G[d] + G[d]) % G[d];
+        return double(g[0] + long(G[0]) * (g[1] + long(G[1]) * g[2]));
+    }
+    bool owned(int x, int y, int z) const
+    {
+        return x >= H && x < H + N && y >= H && y < H + N && z >= H && z < H + N;
+    }
+};
+
+// one rank: its domain, two fields, exchange twice, count bad cells
+long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, int H,
+                         communication_object::options opt, int reps = 2)
+{
+    check_hip(hipSetDevice(0), "hipSetDevice");
+    context ctx(t);
+    const int r = ctx.rank();
+    cube cb{N, H, N + 2 * H, parts, {parts[0] * N, parts[1] * N, parts[2] * N},
+            {r % parts[0], (r / parts[0]) % parts[1], r / (parts[0] * parts[1])}};
+    R::domain_descriptor dom(r, {cb.c[0] * N, cb.c[1] * N, cb.c[2] * N},
+                             {(cb.c[0] + 1) * N - 1, (cb.c[1] + 1) * N - 1, (cb.c[2] + 1) * N - 1});
+    R::halo_generator hg{{0, 0, 0}, {cb.G[0] - 1, cb.G[1] - 1, cb.G[2] - 1}, {H, H, H, H, H, H},
+                         {true, true, true}};
+    auto pattern = R::make_pattern(ctx, hg, {dom});
+    const long E3 = long(cb.E) * cb.E * cb.E;
+    std::vector<double> hd(std::size_t(E3), -1.0);
+    std::vector<float> hf(std::size_t(E3), -1.0f);
+    for (int z = 0; z < cb.E; ++z)
+        for (int y = 0; y < cb.E; ++y)
+            for (int x = 0; x < cb.E; ++x)
+                if (cb.owned(x, y, z))
+                {
+                    hd[std::size_t(cb.idx(x, y, z))] = cb.expect(x, y, z);
+                    hf[std::size_t(cb.idx(x, y, z))] = float(cb.expect(x, y, z) + 1.0);
+                }
+    double* dd = nullptr;
+    float* df = nullptr;
+    check_hip(hipMalloc(&dd, std::size_t(E3) * 8), "hipMalloc");
+    check_hip(hipMalloc(&df, std::size_t(E3) * 4), "hipMalloc");
+    structured::field_descriptor<double, 3> fd(r, dd, {H, H, H}, {cb.E, cb.E, cb.E}, {2, 1, 0});
+    structured::field_descriptor<float, 3> ff(r, df, {H, H, H}, {cb.E, cb.E, cb.E}, {2, 1, 0});
+    communication_object co(ctx, opt);
+    long bad = 0;
+    for (int rep = 0; rep < reps; ++rep)
+    {
+        check_hip(hipMemcpy(dd, hd.data(), std::size_t(E3) * 8, hipMemcpyHostToDevice), "hipMemcpy");
+        check_hip(hipMemcpy(df, hf.data(), std::size_t(E3) * 4, hipMemcpyHostToDevice), "hipMemcpy");
+        auto h = co.exchange(pattern(fd), pattern(ff));
+        h.wait();
+        std::vector<double> od(static_cast<std::size_t>(E3));
+        std::vector<float> of(static_cast<std::size_t>(E3));
+        check_hip(hipMemcpy(od.data(), dd, std::size_t(E3) * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+        check_hip(hipMemcpy(of.data(), df, std::size_t(E3) * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+        for (int z = 0; z < cb.E; ++z)
+            for (int y = 0; y < cb.E; ++y)
+                for (int x = 0; x < cb.E; ++x)
+                {
+                    const double e = cb.expect(x, y, z);
+                    bad += od[std::size_t(cb.idx(x, y, z))] != e;
+                    bad += of[std::size_t(cb.idx(x, y, z))] != float(e + 1.0);
+                }
+    }
+    std::printf("{\"mode\":\"structured\",\"rank\":%d,\"plans\":%zu,\"bad\":%ld}\n", r, co.num_plans(), bad);
+    (void)hipFree(dd);
+    (void)hipFree(df);
+    return bad;
+}
+
+int loopback(int px, int py, int pz, int N, int H)
+{
+    const int n = px * py * pz;
+    loopback_hub hub(n);
+    std::vector<loopback_transport> ts;
+    for (int r = 0; r < n; ++r) ts.emplace_back(hub, r);
+    std::atomic<long> bad{0};
+    std::atomic<int> errors{0};
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; ++r)
+        th.emplace_back([&, r] {
+            try
+            {
+                bad += run_structured_rank(ts[std::size_t(r)], {px, py, pz}, N, H, {});
+            }
+            catch (const std::exception& e)
+            {
+                std::printf("{\"rank\":%d,\"error\":\"%s\"}\n", r, e.what());
+                ++errors;
+            }
+        });
+    for (auto& t : th) t.join();
+    return (bad == 0 && errors == 0) ? 0 : 1;
+}
+
+int rccl(int N, int H, int self)
+{
+    check_hip(hipSetDevice(0), "hipSetDevice");
+    ncclComm_t comm;
+    int dev = 0;
+    check_nccl(ncclCommInitAll(&comm, 1, &dev), "ncclCommInitAll");
+    long bad = 0;
+    {
+        rccl_transport t(comm);
+        communication_object::options opt;
+        opt.self_through_transport = self != 0;
+        bad = run_structured_rank(t, {1, 1, 1}, N, H, opt);
+    }
+    check_nccl(ncclCommDestroy(comm), "ncclCommDestroy");
+    return bad == 0 ? 0 : 1;
+}
+
+int unstructured_case(const char* file, int levels)
+{
+    struct dom
+    {
+        int id;
+        std::vector<std::int64_t> gids, outer;
+    };
+    std::vector<dom> doms;
+    std::ifstream in(file);
+    std::string line;
+    while (std::getline(in, line))
+    {
+        std::istringstream ss(line);
+        dom d;
+        long ng, no;
+        if (!(ss >> d.id >> ng)) continue;
+        d.gids.resize(std::size_t(ng));
+        for (auto& g : d.gids) ss >> g;
+        ss >> no;
+        d.outer.resize(std::size_t(no));
+        for (auto& l : d.outer) ss >> l;
+        doms.push_back(d);
+    }
+    // owner of every gid: the domain where it is an inner cell
+    std::map<std::int64_t, int> owner;
+    for (const auto& d : doms)
+    {
+        std::set<std::int64_t> o(d.outer.begin(), d.outer.end());
+        for (std::size_t l = 0; l < d.gids.size(); ++l)
+            if (!o.count(std::int64_t(l))) owner[d.gids[l]] = d.id;
+    }
+    const int n = int(doms.size());
+    loopback_hub hub(n);
+    std::vector<loopback_transport> ts;
+    for (int r = 0; r < n; ++r) ts.emplace_back(hub, r);
+    std::atomic<long> bad{0};
+    std::atomic<int> errors{0};
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; ++r)
+        th.emplace_back([&, r] {
+            try
+            {
+                check_hip(hipSetDevice(0), "hipSetDevice");
+                context ctx(ts[std::size_t(r)]);
+                const auto& d = doms[std::size_t(r)];
+                unstructured::domain_descriptor ud(d.id, d.gids, d.outer);
+                auto pattern = unstructured::make_pattern(ctx, {}, {ud});
+                const std::size_t ncell = d.gids.size();
+                std::set<std::int64_t> o(d.outer.begin(), d.outer.end());
+                std::vector<double> hv(ncell * std::size_t(levels), -1.0);
+                for (std::size_t l = 0; l < ncell; ++l)
+                    if (!o.count(std::int64_t(l)))
+                        for (int k = 0; k < levels; ++k)
+                            hv[l * std::size_t(levels) + std::size_t(k)] = d.id * 10000.0 + double(d.gids[l]) * 100 + k;
+                double* dv = nullptr;
+                check_hip(hipMalloc(&dv, hv.size() * 8), "hipMalloc");
+                check_hip(hipMemcpy(dv, hv.data(), hv.size() * 8, hipMemcpyHostToDevice), "hipMemcpy");
+                unstructured::data_descriptor<int, double> field(ud, dv, levels, true);
+                communication_object co(ctx);
+                co.exchange(pattern(field)).wait();
+                std::vector<double> out(hv.size());
+                check_hip(hipMemcpy(out.data(), dv, hv.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+                long b = 0;
+                for (std::size_t l = 0; l < ncell; ++l)
+                    for (int k = 0; k < levels; ++k)
+                    {
+                        const int own = o.count(std::int64_t(l)) ? owner.at(d.gids[l]) : d.id;
+                        b += out[l * std::size_t(levels) + std::size_t(k)] != own * 10000.0 + double(d.gids[l]) * 100 + k;
+                    }
+                std::printf("{\"mode\":\"unstructured\",\"rank\":%d,\"bad\":%ld}\n", r, b);
+                bad += b;
+                (void)hipFree(dv);
+            }
+            catch (const std::exception& e)
+            {
+                std::printf("{\"rank\":%d,\"error\":\"%s\"}\n", r, e.what());
+                ++errors;
+            }
+        });
+    for (auto& t : th) t.join();
+    return (bad == 0 && errors == 0) ? 0 : 1;
+}
+
+int bench(int N, int H, int iters)
+{
+    check_hip(hipSetDevice(0), "hipSetDevice");
+    loopback_hub hub(1);
+    loopback_transport t(hub, 0);
+    context ctx(t);
+    const int E = N + 2 * H;
+    R::domain_descriptor dom(0, {0, 0, 0}, {N - 1, N - 1, N - 1});
+    R::halo_generator hg{{0, 0, 0}, {N - 1, N - 1, N - 1}, {H, H, H, H, H, H}, {true, true, true}};
+    auto pattern = R::make_pattern(ctx, hg, {dom});
+    double* dd = nullptr;
+    check_hip(hipMalloc(&dd, std::size_t(E) * E * E * 8), "hipMalloc");
+    check_hip(hipMemset(dd, 0, std::size_t(E) * E * E * 8), "hipMemset");
+    structured::field_descriptor<double, 3> fd(0, dd, {H, H, H}, {E, E, E}, {2, 1, 0});
+    auto co = make_communication_object(ctx);
+    for (int i = 0; i < 10; ++i) co.exchange(pattern(fd)).wait();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; ++i) co.exchange(pattern(fd)).wait();
+    const double us =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
+    const double bytes = 4.0 * (double(E) * E * E - double(N) * N * N) * 8;
+    std::printf("{\"mode\":\"bench\",\"N\":%d,\"H\":%d,\"us_per_exchange\":%.2f,\"GBps\":%.1f}\n", N, H, us,
+                bytes / us / 1e3);
+    (void)hipFree(dd);
+    return 0;
+}
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    try
+    {
+        const std::string mode = argc > 1 ? argv[1] : "";
+        if (mode == "loopback" && argc == 7)
+            return loopback(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                            std::atoi(argv[6]));
+        if (mode == "rccl" && argc == 5) return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
+        if (mode == "unstructured" && argc == 4) return unstructured_case(argv[2], std::atoi(argv[3]));
+        if (mode == "bench" && argc == 5) return bench(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
+    }
+    catch (const std::exception& e)
+    {
+        std::printf("{\"error\":\"%s\"}\n", e.what());
+        return 2;
+    }
+    std::fprintf(stderr, "usage: see the header of co_demo.cpp\n");
+    return 2;
+}

@@ -1,0 +1,104 @@
+"""The C++ communication object (include/ghex_amd/communication_object.hpp): the reference's
+host-side exchange API (context, make_pattern, pattern(field), exchange(...).wait()) in C++ over
+the C ABI, with the loopback transport (ranks as threads on one GPU) and the RCCL transport
+(ncclSend/ncclRecv). Every halo cell is checked against the reference tests' self-validating
+encodings (test/structured/regular/test_regular_domain.cpp:739-800: wrapped global coordinate;
+test/unstructured/unstructured_test_case.hpp:345-388: dom*10000 + gid*100 + level)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "bin", "co_demo")
+INC = os.path.join(ROOT, "include")
+LIB = os.path.join(ROOT, "ghex_amd", "lib")
+
+
+def _run(args, timeout=120):
+    assert os.path.exists(EXE), "build() compiles tests/cpp/bin/co_demo"
+    p = subprocess.run([EXE] + [str(a) for a in args], capture_output=True, text=True,
+                       timeout=timeout)
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+def test_co_header_compiles_host_only(tmp_path):
+    """The header set is plain host C++ (g++, HIP runtime API headers only)."""
+    src = tmp_path / "t.cpp"
+    src.write_text(
+        '#include <ghex_amd/communication_object.hpp>\n'
+        '#include <ghex_amd/field_descriptor.hpp>\n'
+        'int main(){ ghex_amd::loopback_hub hub(2); ghex_amd::loopback_transport t(hub, 1);\n'
+        '  ghex_amd::context ctx(t); ghex_amd::communication_options o; o.fuse_self = false;\n'
+        '  return (ctx.rank() == 1 && ctx.size() == 2 && !o.fuse_self) ? 0 : 1; }\n')
+    exe = tmp_path / "t"
+    subprocess.run(["g++", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", INC, "-I",
+                    "/opt/rocm/include", str(src), "-o", str(exe), "-L", LIB, "-lghx",
+                    "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{LIB}",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    assert subprocess.run([str(exe)]).returncode == 0
+
+
+def test_co_loopback_all_gather_cpu(tmp_path):
+    """make_pattern's setup collective: the loopback all_gather with threads, no GPU."""
+    src = tmp_path / "g.cpp"
+    src.write_text(
+        '#include <ghex_amd/transport.hpp>\n#include <thread>\n'
+        'int main(){ const int n = 5; ghex_amd::loopback_hub hub(n); int bad = 0;\n'
+        '  std::vector<std::thread> th; for (int r = 0; r < n; ++r) th.emplace_back([&, r]{\n'
+        '    ghex_amd::loopback_transport t(hub, r);\n'
+        '    for (int round = 0; round < 50; ++round) {\n'
+        '      std::vector<char> mine(std::size_t(r + round % 3), char(r * 7 + round));\n'
+        '      auto all = t.all_gather(mine);\n'
+        '      for (int q = 0; q < n; ++q) { if (all[q].size() != std::size_t(q + round % 3)) ++bad;\n'
+        '        for (char c : all[q]) if (c != char(q * 7 + round)) ++bad; } } });\n'
+        '  for (auto& t : th) t.join(); return bad ? 1 : 0; }\n')
+    exe = tmp_path / "g"
+    subprocess.run(["g++", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__", "-I", INC, "-I",
+                    "/opt/rocm/include", str(src), "-o", str(exe), "-L/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    assert subprocess.run([str(exe)], timeout=60).returncode == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,N,H", [((1, 1, 1), 12, 2), ((2, 1, 1), 10, 2),
+                                       ((2, 2, 1), 9, 1), ((2, 2, 2), 8, 3),
+                                       ((3, 1, 2), 7, 2)])
+def test_co_loopback_structured(parts, N, H):
+    """PX*PY*PZ ranks (threads) each with one N^3 domain and a double + a float field in one
+    exchange (mixed alignment pads), two exchanges (plan reuse); every cell of every rank."""
+    rc, lines, err = _run(["loopback", *parts, N, H])
+    ranks = [l for l in lines if l.get("mode") == "structured"]
+    assert rc == 0, (lines, err)
+    assert len(ranks) == parts[0] * parts[1] * parts[2]
+    assert all(l["bad"] == 0 and l["plans"] == 1 for l in ranks)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("self_through", [0, 1])
+def test_co_rccl_single_rank(self_through):
+    """RCCL transport: with SELF=1 the 26 self messages travel through ncclSend/ncclRecv to self
+    inside one group (the rccl_transport code path on one GPU); SELF=0 the fused self launch."""
+    rc, lines, err = _run(["rccl", 12, 2, self_through])
+    assert rc == 0, (lines, err)
+    assert [l["bad"] for l in lines if l.get("mode") == "structured"] == [0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("levels", [1, 3])
+def test_co_loopback_unstructured_known_answer(tmp_path, levels):
+    """The reference's 4-domain unstructured case (unstructured_test_case.hpp:35-86), one domain
+    per rank (threads), data_descriptor levels_first: every halo value = its owner's encoding."""
+    case = json.load(open(os.path.join(ROOT, "tests", "golden", "unstructured_case.json")))
+    f = tmp_path / "doms.txt"
+    with open(f, "w") as fh:
+        for i in sorted(case["domains"], key=int):
+            d = case["domains"][i]
+            fh.write(" ".join(str(x) for x in [i, len(d["gids"]), *d["gids"], len(d["halo_lids"]),
+                                               *d["halo_lids"]]) + "\n")
+    rc, lines, err = _run(["unstructured", str(f), levels])
+    assert rc == 0, (lines, err)
+    ranks = [l for l in lines if l.get("mode") == "unstructured"]
+    assert len(ranks) == 4 and all(l["bad"] == 0 for l in ranks)
