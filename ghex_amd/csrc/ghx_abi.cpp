@@ -431,6 +431,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || (value & 15)) throw invalid("self_chunk must be a multiple of 16 (0: tile)");
             g_tune.self_chunk = uint32_t(value);
         }
+        else if (k == "self_pipe")
+        {
+            if (value < 0 || value > 2) throw invalid("self_pipe must be 0, 1 or 2");
+            g_tune.self_pipe = value;
+        }
         else if (k == "xcd_pair")
         {
             if (value < 0 || value > 1) throw invalid("xcd_pair must be 0 or 1");
@@ -962,6 +967,8 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
         a.segs = p.dev.segs;
         a.segs2 = q.dev.segs;
         a.chunk = g_tune.self_chunk;
+        // 1: short-row (x-face) tiles only, 2: every tile
+        a.pipe = g_tune.self_pipe == 2 ? 0xFFFFFFFFu : g_tune.self_pipe ? g_tune.small_row_bytes : 0u;
         a.tile_seg = p.dev.tiles;
         a.n_tiles = p.n_tiles;
         for (int i = 0; i <= p.max_field_slot; ++i)

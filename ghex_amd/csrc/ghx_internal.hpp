@@ -52,6 +52,10 @@ struct tuning
     uint32_t self_chunk = 0;           // fused self exchange: a workgroup packs, then unpacks,
                                        // this many buffer bytes at a time (0: the whole tile;
                                        // 4-32 KiB chunks measured no faster, 4 KiB slower)
+    int self_pipe = 0;                 // fused self exchange: software-pipelined tiles (the
+                                       // x-face halo stores overlap the next chunk's loads);
+                                       // 1 short-row tiles, 2 all. Measured: H=2 within noise,
+                                       // H=1 +3 %, H=3 +12 % time -> off
     int xcd_pair = 1;                  // dispatch the tiles of line-sharing short-row segment
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt
@@ -140,6 +144,9 @@ struct kargs
     const uint32_t* tile_seg;  // per tile: {segment index, tile index within the segment}
     uint32_t n_tiles;
     uint32_t chunk;            // fused self exchange: pack/unpack alternate per chunk (0: tile)
+    uint32_t pipe;             // fused self exchange: tiles with rows shorter than this many
+                               // bytes are software-pipelined (self_pipelined)
+    uint32_t pad0;
     uint64_t field_ptr[GHX_MAX_SLOTS];
     uint64_t buf_ptr[GHX_MAX_SLOTS];
 };

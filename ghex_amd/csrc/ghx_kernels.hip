@@ -399,6 +399,78 @@ __device__ __forceinline__ void copy_any(const seg_s& s, char* field, char* buf,
     }
 }
 
+// Software-pipelined self tile (pack and unpack of one tile with the same vector width W): trip j
+// loads the field rows of chunk j (pack) and the buffer bytes of chunk j-1 (unpack), stores
+// chunk j to the buffer, waits for ITS OWN memory operations, passes the workgroup barrier (chunk
+// j's buffer bytes are then complete for every wave), and only then stores chunk j-1 into the
+// halos. Those halo stores — the scattered writes of the x-faces — are left in flight under the
+// next trip's scattered field loads instead of being drained by every barrier, so the x-face reads
+// and writes overlap inside each workgroup (with plain __syncthreads between a whole pack half and
+// a whole unpack half, all x-face workgroups read, then all of them write).
+template<int W, int U>
+__device__ __forceinline__ void self_pipelined(const seg_s& s, const seg_s& q,
+                                               char* __restrict__ fp, char* __restrict__ fu,
+                                               char* __restrict__ buf, uint32_t start,
+                                               uint32_t end)
+{
+    using V = typename vec_t<W>::type;
+    constexpr uint32_t K = uint32_t(U) * kBlock * W;  // buffer bytes per trip
+    const uint32_t lane = threadIdx.x * W;
+    const uint32_t pol_p = s.fpol, pol_u = q.fpol;
+    const uint32_t n = (end - start + K - 1) / K;
+    for (uint32_t j = 0; j <= n; ++j)
+    {
+        const uint32_t cp = start + j * K;  // pack chunk (j < n)
+        const uint32_t cu = cp - K;         // unpack chunk (j > 0)
+        V pv[U], uv[U];
+        int64_t fo[U];
+        if (j < n)
+        {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+            {
+                const uint32_t p = cp + uint32_t(u) * kBlock * W + lane;
+                if (p < end) pv[u] = fload<V, false>(fp + field_offset_s(s, p), pol_p);
+            }
+        }
+        if (j > 0)
+        {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+            {
+                const uint32_t p = cu + uint32_t(u) * kBlock * W + lane;
+                if (p < end)
+                {
+                    uv[u] = vload<V, false>(buf + p);
+                    fo[u] = field_offset_s(q, p);
+                }
+            }
+        }
+        if (j < n)
+        {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+            {
+                const uint32_t p = cp + uint32_t(u) * kBlock * W + lane;
+                if (p < end) vstore<V, false>(buf + p, pv[u]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's buffer stores landed
+        __builtin_amdgcn_s_barrier();                      // ... and every other wave's
+        if (j > 0)
+        {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+            {
+                const uint32_t p = cu + uint32_t(u) * kBlock * W + lane;
+                if (p < end) fstore<V, false>(fu + fo[u], uv[u], pol_u);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // lanes are reused by the next tile of a grid-stride loop
+}
+
 // Fused self exchange: every message is a self message, so pack segment k and unpack segment k
 // cover the same buffer bytes. A workgroup packs its tile (field interior -> buffer), waits at a
 // workgroup barrier (its own stores are visible to its own waves), then unpacks the same bytes
@@ -423,6 +495,18 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
         wp = min(wp, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
         int wu = min(int(q.wlog2), ptr_wlog2(reinterpret_cast<uint64_t>(field_u)));
         wu = min(wu, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+        if (a.pipe && wp == wu && s.row_bytes < a.pipe)
+        {
+            switch (wp)
+            {
+                case 4: self_pipelined<16, U>(s, q, field_p, field_u, buf, start, end); break;
+                case 3: self_pipelined<8, U>(s, q, field_p, field_u, buf, start, end); break;
+                case 2: self_pipelined<4, U>(s, q, field_p, field_u, buf, start, end); break;
+                case 1: self_pipelined<2, U>(s, q, field_p, field_u, buf, start, end); break;
+                default: self_pipelined<1, U>(s, q, field_p, field_u, buf, start, end); break;
+            }
+            continue;
+        }
         // Whole tile, or in chunks of a.chunk buffer bytes (g_tune.self_chunk, a knob: keeping
         // the re-read bytes in L2 this way measured no faster).
         const uint32_t chunk = a.chunk ? a.chunk : s.tile_bytes;
