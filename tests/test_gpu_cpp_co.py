@@ -77,6 +77,17 @@ def test_co_loopback_structured(parts, N, H):
 
 
 @pytest.mark.gpu
+def test_co_loopback_config3_geometry():
+    """BASELINE config 3's decomposition (2x2x2 periodic, 7 peers per rank: 8 MiB faces, 64 KiB
+    edges, 512 B corners at 512^3) as 8 thread-ranks on one GPU at 256^3 per rank (512^3 per
+    rank also passes: `co_demo loopback 2 2 2 512 2`); every cell of every rank."""
+    rc, lines, err = _run(["loopback", 2, 2, 2, 256, 2], timeout=300)
+    ranks = [l for l in lines if l.get("mode") == "structured"]
+    assert rc == 0, (lines, err)
+    assert len(ranks) == 8 and all(l["bad"] == 0 for l in ranks)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("self_through", [0, 1])
 def test_co_rccl_single_rank(self_through):
     """RCCL transport: with SELF=1 the 26 self messages travel through ncclSend/ncclRecv to self
