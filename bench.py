@@ -199,14 +199,23 @@ def main():
     run(args.warmup)
     torch.cuda.synchronize(dev)
 
-    def timed(fn, k):
+    dev_time = {}
+
+    def timed(fn, k, events=False):
+        """Host wall time of k calls (barrier + synchronize on both sides, max over ranks); with
+        events=True also the device time of the region from HIP events on the launch stream."""
         if distributed:
             dist.barrier(device_ids=[local])
         torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        e0.record(stream)
         for _ in range(k):
             fn()
+        e1.record(stream)
         torch.cuda.synchronize(dev)
+        if events:
+            dev_time["s"] = e0.elapsed_time(e1) * 1e-3
         if distributed:
             dist.barrier(device_ids=[local])
         dt = time.perf_counter() - t0
@@ -219,7 +228,8 @@ def main():
     K = args.steps
     run(K % max(1, args.steps_per_graph) or 1)  # instantiate the remainder graph untimed
     torch.cuda.synchronize(dev)
-    T = timed(lambda: run(K), 1)
+    T = timed(lambda: run(K), 1, events=True)
+    dev_step = dev_time["s"] / K  # device time per step over the timed region (HIP events)
     value = world * step_bytes * K / T / 1e9
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
@@ -246,11 +256,15 @@ def main():
     # rounds; pack = T1 - T0, unpack = T2 - T1 (each includes its dependent-launch boundary).
     t_pack, t_unpack = kernel_durations(torch, dev, stream, [pack, unpack])
     if use_fused:
+        # one launch per step: its average duration over the timed region = device time / K
         (t_fused,) = kernel_durations(torch, dev, stream, [fused])
-        launch_bytes, dom_name, dom_t, kname = step_bytes, "self", t_fused, "k_self (pack+unpack)"
+        launch_bytes, dom_name, dom_t, kname = step_bytes, "self", dev_step, "k_self (pack+unpack)"
     else:
+        # two launches per step: the timed region's device time split by their live differential
+        # durations (graphs of M and M+1 launches)
         launch_bytes = 2 * n_halo * 8
-        dom_name, dom_t = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+        dom_name, dom_d = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+        dom_t = dev_step * dom_d / (t_pack + t_unpack)
         kname = f"k_copy<{dom_name}>"
     achieved = launch_bytes / dom_t / 1e9
     traffic = None
@@ -267,7 +281,14 @@ def main():
                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                        "algorithmic_bytes_per_launch": launch_bytes,
                        "launch_us": round(dom_t * 1e6, 2),
+                       "launch_us_source": "HIP events on the launch stream around the timed "
+                                           "region, device time per step" +
+                                           ("" if use_fused else " x the kernel's share of the "
+                                            "step (graph differencing)"),
+                       "step_device_us": round(dev_step * 1e6, 2),
                        "pack_us": round(t_pack * 1e6, 2), "unpack_us": round(t_unpack * 1e6, 2)}
+    if use_fused:
+        out["roofline"]["self_us_differential"] = round(t_fused * 1e6, 2)
     if use_fused:
         # the same step as two launches (what N>1 runs per rank), for comparison
         run_u = make_run(step_unfused)
