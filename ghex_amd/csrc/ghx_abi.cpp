@@ -436,6 +436,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 2) throw invalid("self_pipe must be 0, 1 or 2");
             g_tune.self_pipe = value;
         }
+        else if (k == "self_lane_local")
+        {
+            if (value < 0 || value > 1) throw invalid("self_lane_local must be 0 or 1");
+            g_tune.self_lane_local = value;
+        }
         else if (k == "xcd_pair")
         {
             if (value < 0 || value > 1) throw invalid("xcd_pair must be 0 or 1");
@@ -967,6 +972,7 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
         a.segs = p.dev.segs;
         a.segs2 = q.dev.segs;
         a.chunk = g_tune.self_chunk;
+        a.lane_local = uint32_t(g_tune.self_lane_local);
         // 1: short-row (x-face) tiles only, 2: every tile
         a.pipe = g_tune.self_pipe == 2 ? 0xFFFFFFFFu : g_tune.self_pipe ? g_tune.small_row_bytes : 0u;
         a.tile_seg = p.dev.tiles;

@@ -30,9 +30,10 @@ struct tuning
     int nt = 0;                     // 0 default, 1 nt stores, 2 nt loads + stores, 3 nt loads
     int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
     uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
-    uint32_t self_tile_bytes = 4096;   // the same for the fused self exchange (k_self: each
-                                       // tile is packed, then unpacked by one workgroup;
-                                       // measured best 4 KiB vs 8 KiB for two launches)
+    uint32_t self_tile_bytes = kTileBytes;  // the same for the fused self exchange (separate
+                                       // self plans are built when it differs; with the
+                                       // barrier-free self tiles 8 KiB measured best: 4 KiB
+                                       // +0-7 %)
     uint32_t small_tile_rows = 4096;   // rows per tile of segments with short rows
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
@@ -56,6 +57,8 @@ struct tuning
                                        // x-face halo stores overlap the next chunk's loads);
                                        // 1 short-row tiles, 2 all. Measured: H=2 within noise,
                                        // H=1 +3 %, H=3 +12 % time -> off
+    int self_lane_local = 1;           // fused self exchange without the intra-tile barrier
+                                       // when both halves use the same vector width
     int xcd_pair = 1;                  // dispatch the tiles of line-sharing short-row segment
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt
@@ -146,7 +149,8 @@ struct kargs
     uint32_t chunk;            // fused self exchange: pack/unpack alternate per chunk (0: tile)
     uint32_t pipe;             // fused self exchange: tiles with rows shorter than this many
                                // bytes are software-pipelined (self_pipelined)
-    uint32_t pad0;
+    uint32_t lane_local;       // fused self exchange: no barrier when pack and unpack of a tile
+                               // map lanes to buffer bytes identically
     uint64_t field_ptr[GHX_MAX_SLOTS];
     uint64_t buf_ptr[GHX_MAX_SLOTS];
 };

@@ -509,6 +509,18 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
         }
         // Whole tile, or in chunks of a.chunk buffer bytes (g_tune.self_chunk, a knob: keeping
         // the re-read bytes in L2 this way measured no faster).
+        if (wp == wu && a.lane_local)
+        {
+            // Same vector width on both sides: every lane unpacks exactly the buffer bytes it
+            // packed (same lane -> position map), so the hand-off is program order within the
+            // lane (its own stores, then its own loads of the same addresses) and no workgroup
+            // barrier is needed: waves run free, and one wave's halo writes overlap other waves'
+            // field reads instead of every wave of the tile reading first and writing after.
+            copy_any<true, U, NT>(s, field_p, buf, start, end, wp);
+            asm volatile("" ::: "memory");  // keep the unpack's buffer loads after the stores
+            copy_any<false, U, NT>(q, field_u, buf, start, end, wu);
+            continue;
+        }
         const uint32_t chunk = a.chunk ? a.chunk : s.tile_bytes;
         for (uint32_t c = start; c < end; c += chunk)
         {

@@ -97,3 +97,22 @@ def test_fused_equals_unfused_and_oracle(Hw, layout):
     for field, buf in outs:
         np.testing.assert_array_equal(field, a)
         np.testing.assert_array_equal(buf, ob)
+
+
+@pytest.mark.parametrize("knobs", [{"self_lane_local": 0}, {"self_tile_bytes": 4096},
+                                   {"self_tile_bytes": 2048, "self_lane_local": 0,
+                                    "self_chunk": 1024},
+                                   {"self_pipe": 1}, {"self_pipe": 2, "unroll": 2},
+                                   {"unroll": 8, "xcd_pair": 0}])
+@pytest.mark.parametrize("Hw", [1, 2, 3])
+def test_self_kernel_variants_stay_bit_exact(knobs, Hw):
+    """Every variant of the fused self kernel (barrier / lane-local hand-off, tile and chunk
+    sizes, software pipelining, unroll) writes the oracle's buffer bytes and halos."""
+    from ghex_amd import _ghx
+    try:
+        for k, v in knobs.items():
+            _ghx.call("ghx_tune", k.encode(), v)
+        test_fused_equals_unfused_and_oracle(Hw, (2, 1, 0))
+        test_fused_equals_unfused_and_oracle(Hw, (0, 2, 1))
+    finally:
+        _ghx.call("ghx_tune", b"reset", 0)
