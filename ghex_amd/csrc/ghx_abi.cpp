@@ -451,6 +451,16 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 1) throw invalid("u_tile_rows must be >= 1");
             g_tune.u_tile_rows = uint32_t(value);
         }
+        else if (k == "urun")
+        {
+            if (value < 0 || value > 1) throw invalid("urun must be 0 or 1");
+            g_tune.urun = value;
+        }
+        else if (k == "u_run_tile_rows")
+        {
+            if (value < 4) throw invalid("u_run_tile_rows must be >= 4");
+            g_tune.u_run_tile_rows = uint32_t(value);
+        }
         else if (k == "usort")
         {
             if (value < 0 || value > 1) throw invalid("usort must be 0 or 1");

@@ -44,6 +44,9 @@ struct tuning
                                        // y+1 share a cache line): one lane moves both. Off by
                                        // default: with short-row-first dispatch the L2 already
                                        // merges the shared-line misses (same TCC_EA0_RDREQ)
+    int urun = 1;                      // unstructured 4/8-B-row segments: 16-B lane chunks with
+                                       // run detection (copy_runs)
+    uint32_t u_run_tile_rows = 2048;   // rows per tile of run-heavy index-list segments
     int usort = 0;                     // unstructured one-row-per-index segments: visit the
                                        // indices in ascending field order (buffer side
                                        // scattered through a permutation)
@@ -136,6 +139,11 @@ struct alignas(16) seg_u
     uint8_t fpol;              // field-side cache policy (as seg_s)
     uint32_t tile_bytes;
     const uint32_t* perm;      // mode 0, sorted: lids ascending, perm[k] = buffer row of lid k
+    uint8_t runs;              // mode 0, rows of 4 or 8 B, rows of consecutive lids contiguous
+                               // in the field: lanes move 16-B chunks (16/L rows), one 16-B
+                               // field access where the chunk's lids form a run (copy_runs);
+                               // 2: at least half the chunks are runs (u_run_tile_rows tiles)
+    uint8_t pad2[7];
 };
 static_assert(sizeof(seg_u) == 96, "seg_u layout");
 
@@ -161,7 +169,7 @@ const char* get_error();
 
 // kernel launchers (ghx_kernels.hip)
 int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid);
-int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid);
+int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid, bool runs);
 int launch_self(const kargs& a, void* stream, uint32_t grid);
 int launch_put(const kargs& a, void* stream, uint32_t grid);
 uint32_t grid_for_tiles(uint32_t n_tiles);

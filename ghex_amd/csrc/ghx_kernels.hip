@@ -18,6 +18,8 @@
 // NT = cache policy (0 default, 1 non-temporal stores, 2 non-temporal loads and stores).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ghx_internal.hpp"
 
 namespace ghx
@@ -251,6 +253,167 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
     }
 }
 
+// Unstructured rows of L = 4 or 8 bytes with run detection (seg_u::runs): lane t of a wave moves
+// the 16-B buffer chunk [p, p+16) = rows r0 .. r0+K-1 (K = 16/L). It loads the chunk's K lids
+// with one vector load and tests whether they form a run (lid[j] = lid[0] + j): then the K rows
+// are 16 contiguous field bytes and move as ONE 16-B field access; otherwise as K L-byte
+// accesses assembled into the same 16-B buffer vector. The buffer side is a lane-linear
+// 16 B/lane stream either way (the one-row-per-lane path moves 4-8 B per lane instruction).
+// A wave whose lids are all runs issues the per-row instructions with an empty EXEC mask, which
+// the hardware skips; mixed waves execute both, masked. Field accesses of a run are only
+// L-aligned: the HSA runtime runs kernels in unaligned-access mode, so a 16-B access at a 4-B
+// aligned address is legal (split by the TA where it crosses a line).
+using v4_a4 = unsigned __attribute__((ext_vector_type(4), aligned(4)));
+
+template<int K>
+__device__ __forceinline__ void load_lids(const seg_u& s, uint32_t r0, int64_t (&l)[K])
+{
+    if (s.lid64)
+    {
+        const GHX_GLOBAL vec_t<16>::type* p =
+            (const GHX_GLOBAL vec_t<16>::type*)((const int64_t*)(s.lids) + r0);
+#pragma unroll
+        for (int j = 0; j < K; j += 2)
+        {
+            const auto q = p[j / 2];
+            l[j] = int64_t(uint64_t(q.x) | (uint64_t(q.y) << 32));
+            l[j + 1] = int64_t(uint64_t(q.z) | (uint64_t(q.w) << 32));
+        }
+    }
+    else if constexpr (K == 2)
+    {
+        const auto q = *(const GHX_GLOBAL vec_t<8>::type*)((const int32_t*)(s.lids) + r0);
+        l[0] = int32_t(q.x);
+        l[1] = int32_t(q.y);
+    }
+    else
+    {
+        const auto q = *(const GHX_GLOBAL vec_t<16>::type*)((const int32_t*)(s.lids) + r0);
+        l[0] = int32_t(q.x);
+        l[1] = int32_t(q.y);
+        l[2] = int32_t(q.z);
+        l[3] = int32_t(q.w);
+    }
+}
+
+template<int L>
+__device__ __forceinline__ vec_t<16>::type assemble(const typename vec_t<L>::type (&w)[16 / L])
+{
+    if constexpr (L == 8) return vec_t<16>::type{w[0].x, w[0].y, w[1].x, w[1].y};
+    else return vec_t<16>::type{w[0], w[1], w[2], w[3]};
+}
+
+template<int L>
+__device__ __forceinline__ void split(vec_t<16>::type v, typename vec_t<L>::type (&w)[16 / L])
+{
+    if constexpr (L == 8)
+    {
+        w[0] = vec_t<8>::type{v.x, v.y};
+        w[1] = vec_t<8>::type{v.z, v.w};
+    }
+    else
+    {
+        w[0] = v.x;
+        w[1] = v.y;
+        w[2] = v.z;
+        w[3] = v.w;
+    }
+}
+
+template<bool PACK, int L, int U, int NT>
+__device__ __forceinline__ void copy_runs(const seg_u& s, char* __restrict__ field,
+                                          char* __restrict__ buf, uint32_t start, uint32_t end)
+{
+    using V = typename vec_t<16>::type;
+    using R = typename vec_t<L>::type;
+    constexpr int K = 16 / L;
+    constexpr bool NTL = NT >= 2;
+    constexpr bool NTS = NT == 1 || NT == 2;
+    const uint32_t pol = s.fpol;
+    for (uint32_t base = start + threadIdx.x * 16; base < end; base += U * kBlock * 16)
+    {
+        int64_t fo[U][K];
+        uint32_t full = 0, run = 0;  // bit u: chunk u holds K rows / ... that form a run
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * 16;
+            if (p >= end) continue;
+            const uint32_t r0 = p / L;
+            int64_t l[K];
+            if (p + 16 <= end)
+            {
+                full |= 1u << u;
+                load_lids<K>(s, r0, l);
+                bool c = true;
+#pragma unroll
+                for (int j = 1; j < K; ++j) c = c && l[j] == l[0] + j;
+                if (c) run |= 1u << u;
+            }
+            else
+            {
+#pragma unroll
+                for (int j = 0; j < K; ++j) l[j] = p + j * L < end ? load_lid(s, r0 + j) : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) fo[u][j] = l[j] * L;  // index stride = L (planner)
+        }
+        V v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * 16;
+            if (p >= end || !(full >> u & 1u)) continue;
+            if (PACK)
+            {
+                if (run >> u & 1u)
+                {
+                    const v4_a4 x = fload<v4_a4, NTL>(field + fo[u][0], pol);
+                    v[u] = V{x.x, x.y, x.z, x.w};
+                }
+                else
+                {
+                    R w[K];
+#pragma unroll
+                    for (int j = 0; j < K; ++j) w[j] = fload<R, NTL>(field + fo[u][j], pol);
+                    v[u] = assemble<L>(w);
+                }
+            }
+            else
+                v[u] = vload<V, NTL>(buf + p);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = base + u * kBlock * 16;
+            if (p >= end) continue;
+            if (!(full >> u & 1u))
+            {
+                // segment tail: fewer than K rows left, row by row
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                {
+                    if (p + j * L >= end) break;
+                    if (PACK) vstore<R, NTS>(buf + p + j * L, fload<R, NTL>(field + fo[u][j], pol));
+                    else fstore<R, NTS>(field + fo[u][j], vload<R, NTL>(buf + p + j * L), pol);
+                }
+                continue;
+            }
+            if (PACK)
+                vstore<V, NTS>(buf + p, v[u]);
+            else if (run >> u & 1u)
+                fstore<v4_a4, NTS>(field + fo[u][0], v4_a4{v[u].x, v[u].y, v[u].z, v[u].w}, pol);
+            else
+            {
+                R w[K];
+                split<L>(v[u], w);
+#pragma unroll
+                for (int j = 0; j < K; ++j) fstore<R, NTS>(field + fo[u][j], w[j], pol);
+            }
+        }
+    }
+}
+
 // Paired segments (planner: pair_segments): lane moves row r of the primary and row r-1 of the
 // partner, whose field pieces share a cache line; both buffer streams stay lane-linear.
 template<bool PACK, int W, int U, int NT>
@@ -357,7 +520,10 @@ __device__ __forceinline__ int ptr_wlog2(uint64_t p)
     return __builtin_ctzll(p | 16ull);  // log2 of the largest power of two (<= 16) dividing p
 }
 
-template<bool PACK, int U, int NT, typename Seg>
+// RUNS (unstructured only): every segment of the plan takes the run path (copy_runs); the host
+// (uplan::execute) launches this variant only when runs_ok holds for all of them, so the
+// general path's registers do not weigh on it and vice versa.
+template<bool PACK, int U, int NT, typename Seg, bool RUNS = false>
 __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
 {
     const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
@@ -373,6 +539,12 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         int w = s.wlog2;
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+        if constexpr (RUNS)
+        {
+            if (s.row_bytes == 8) copy_runs<PACK, 8, U, NT>(s, field, buf, start, end);
+            else copy_runs<PACK, 4, U, NT>(s, field, buf, start, end);
+            continue;
+        }
         if (try_pair<PACK, U, NT>(s, segs, a, field, buf, start, end, w)) continue;
         switch (w)
         {
@@ -668,11 +840,15 @@ int launch_put(const kargs& a, void* stream, uint32_t grid)
     return GHX_OK;
 }
 
-int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid)
+int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid, bool runs)
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (direction == 0) launch_variant<seg_u, true>(a, s, grid);
+    if (runs && direction == 0)
+        hipLaunchKernelGGL((k_copy<true, 4, 0, seg_u, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (runs)
+        hipLaunchKernelGGL((k_copy<false, 4, 0, seg_u, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (direction == 0) launch_variant<seg_u, true>(a, s, grid);
     else launch_variant<seg_u, false>(a, s, grid);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)

@@ -60,6 +60,16 @@ std::vector<int32_t> line_partners(const std::vector<seg_u>& segs)
     return std::vector<int32_t>(segs.size(), -1);
 }
 
+// Rows per tile of a short-row segment: structured short rows want few large tiles (measured
+// best: 4096 rows); index-list gathers are latency-bound random accesses and want many
+// workgroups in flight (512 rows), except run-heavy lists on the run path, which stream
+// (2048 rows: tools/urun_bench.py, contiguous lids 40 -> 33 us).
+uint32_t short_tile_rows(const seg_s&) { return g_tune.small_tile_rows; }
+uint32_t short_tile_rows(const seg_u& s)
+{
+    return s.runs == 2 ? g_tune.u_run_tile_rows : g_tune.u_tile_rows;
+}
+
 // Tile table: per tile {segment, tile index within the segment}. Segments with short rows
 // (request-bound: one memory request per row) may use a different tile size from streaming
 // segments; the dispatch order of tiles is a tuning knob (hardware dispatches in blockIdx order).
@@ -76,8 +86,7 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
         {
             // structured short rows: few large tiles (measured best: 4096 rows); index-list
             // gathers are latency-bound random accesses and want many workgroups in flight
-            const uint32_t rows = std::is_same<Seg, seg_u>::value ? g_tune.u_tile_rows
-                                                                  : g_tune.small_tile_rows;
+            const uint32_t rows = short_tile_rows(segs[i]);
             const uint64_t want = uint64_t(rows) * segs[i].row_bytes;
             tb = uint32_t(std::max<uint64_t>(segs[i].row_bytes, std::min<uint64_t>(want, kMaxTileBytes)));
             tb -= tb % segs[i].row_bytes;  // whole rows per tile
@@ -524,6 +533,23 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         if (en.n_lids > 1) w = std::min(w, wlog2_of(uint64_t(s.index_stride_b < 0 ? -s.index_stride_b : s.index_stride_b)));
         if (s.mode != 0) w = std::min(w, wlog2_of(uint64_t(s.level_stride_b < 0 ? -s.level_stride_b : s.level_stride_b)));
         s.wlog2 = uint8_t(w);
+        // 4/8-B rows whose consecutive lids are adjacent in the field (index stride = row
+        // length): 16-B lane chunks, one field access per run of 16/L lids (copy_runs)
+        s.runs = (g_tune.urun && s.mode == 0 && (L == 4 || L == 8) && s.index_stride_b == L &&
+                  s.buf_off % 16 == 0) ? 1 : 0;
+        if (s.runs)
+        {
+            // run-heavy: at least half of the 16-B chunks hold 16/L consecutive lids
+            const int64_t K = 16 / L, chunks = en.n_lids / K;
+            int64_t hits = 0;
+            for (int64_t c = 0; c < chunks; ++c)
+            {
+                bool run = true;
+                for (int64_t j = 1; j < K && run; ++j) run = en.lids[c * K + j] == en.lids[c * K] + j;
+                hits += run ? 1 : 0;
+            }
+            if (chunks > 0 && 2 * hits >= chunks) s.runs = 2;
+        }
         lid_bytes = (lid_bytes + 15) & ~size_t(15);
         pending pe{segs.size(), en.lids, en.n_lids, wide, lid_bytes};
         lid_bytes += size_t(en.n_lids) * (wide ? 8 : 4);
@@ -531,6 +557,7 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
             !std::is_sorted(en.lids, en.lids + en.n_lids))
         {
             lid_bytes = (lid_bytes + 15) & ~size_t(15);
+            s.runs = 0;  // the buffer side goes through perm
             pe.sorted = true;
             pe.perm_off = lid_bytes;
             lid_bytes += size_t(en.n_lids) * 4;
@@ -542,6 +569,7 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
     std::vector<uint32_t> tiles = build_tiles(segs);
     n_segments = int32_t(segs.size());
     n_tiles = uint32_t(tiles.size() / 2);
+    host_segs = segs;
     if (!segs.empty() && have_device())
     {
         std::vector<unsigned char> host(lid_bytes);
@@ -603,7 +631,14 @@ int uplan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
         if (!bptr[i]) throw invalid("null buffer pointer");
         a.buf_ptr[i] = reinterpret_cast<uint64_t>(bptr[i]);
     }
-    return launch_unstructured(a, direction, stream, grid_for_tiles(n_tiles));
+    // the run-path kernel when every segment qualifies with these pointers: flagged by the
+    // planner, whole 16-B chunks per tile, 16-B aligned buffer ranges, field base aligned to L
+    bool runs = !host_segs.empty();
+    for (const seg_u& s : host_segs)
+        runs = runs && s.runs && s.tile_bytes % 16 == 0 &&
+               (a.buf_ptr[s.buf_slot] + s.buf_off) % 16 == 0 &&
+               a.field_ptr[s.field_slot] % s.row_bytes == 0;
+    return launch_unstructured(a, direction, stream, grid_for_tiles(n_tiles), runs);
 }
 
 }  // namespace ghx

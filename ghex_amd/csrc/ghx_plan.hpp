@@ -59,6 +59,7 @@ struct uplan
     uint32_t tile_bytes = kTileBytes;
     int max_field_slot = -1, max_buf_slot = -1;
     device_tables dev;
+    std::vector<seg_u> host_segs;  // for the launch-time choice of the run-path kernel
     uplan(const ghx_upack_entry* entries, int n_entries, int direction);
     int execute(void* const* fptr, int nf, void* const* bptr, int nb, void* stream) const;
 };

@@ -4,7 +4,8 @@ ballot/prefix run detection (contiguous lid runs -> wider per-lane vectors)?
 
 The product kernel (k_copy<seg_u>, one lane per 8-B row at levels=1 fp64) is timed on one index
 list shape per line — pack (gather into a buffer) + unpack (scatter back) of n indices of a
-10M-cell fp64 field, hipGraph-replayed — next to a plain device copy of the same bytes:
+10M-cell fp64 field, hipGraph-replayed — next to a plain device copy of the same bytes (argv:
+ghx_tune settings "key=v,key=v", one pass over the shapes each):
   random    : n distinct random lids (BASELINE config 5's shape)
   sorted    : the same lids ascending (field side in address order)
   runs64    : runs of 64 consecutive lids at random run starts
@@ -63,6 +64,7 @@ def main():
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / (reps * per)
 
+    tunes = sys.argv[1:] or [""]
     for n in (500_000, 4_000_000):
         shapes = {}
         r = rng.choice(ncells, size=n, replace=False)
@@ -79,7 +81,11 @@ def main():
         dst = torch.empty_like(src)
         t_copy = graph_time(lambda s: (dst.copy_(src), src.copy_(dst)))
         ref = 4 * n * 8 / t_copy / 1e9
-        for name, lids in shapes.items():
+        for tune, (name, lids) in ((t, x) for t in tunes for x in shapes.items()):
+            _ghx.call("ghx_tune", b"reset", 0)
+            for kv in filter(None, tune.split(",")):
+                k, v = kv.split("=")
+                _ghx.call("ghx_tune", k.encode(), int(v))
             hp, hu = plan(lids, 0), plan(lids, 1)
 
             def step(s):
@@ -89,7 +95,7 @@ def main():
             L.ghx_uplan_destroy(hp)
             L.ghx_uplan_destroy(hu)
             lines = len(np.unique(np.asarray(lids) * 8 // 128))
-            print(json.dumps({"n": n, "lids": name, "us": round(t * 1e6, 2),
+            print(json.dumps({"tune": tune, "n": n, "lids": name, "us": round(t * 1e6, 2),
                               "GBps": round(4 * n * 8 / t / 1e9, 1),
                               "copy_GBps_same_bytes": round(ref, 1),
                               "field_lines": lines}), flush=True)
