@@ -168,7 +168,7 @@ void set_error(const std::string& msg);
 const char* get_error();
 
 // kernel launchers (ghx_kernels.hip)
-int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid);
+int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid, bool pairs);
 int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid, bool runs);
 int launch_self(const kargs& a, void* stream, uint32_t grid);
 int launch_put(const kargs& a, void* stream, uint32_t grid);

@@ -522,8 +522,10 @@ __device__ __forceinline__ int ptr_wlog2(uint64_t p)
 
 // RUNS (unstructured only): every segment of the plan takes the run path (copy_runs); the host
 // (uplan::execute) launches this variant only when runs_ok holds for all of them, so the
-// general path's registers do not weigh on it and vice versa.
-template<bool PACK, int U, int NT, typename Seg, bool RUNS = false>
+// general path's registers do not weigh on it and vice versa. PAIR (structured only): the plan
+// holds paired segments (knob "pair"); the pair path more than doubles the kernel's VGPRs
+// (156 vs 73 at U=4), so plans without pairs launch the variant that leaves it out.
+template<bool PACK, int U, int NT, typename Seg, bool RUNS = false, bool PAIR = false>
 __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
 {
     const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
@@ -545,7 +547,10 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
             else copy_runs<PACK, 4, U, NT>(s, field, buf, start, end);
             continue;
         }
-        if (try_pair<PACK, U, NT>(s, segs, a, field, buf, start, end, w)) continue;
+        if constexpr (PAIR)
+        {
+            if (try_pair<PACK, U, NT>(s, segs, a, field, buf, start, end, w)) continue;
+        }
         switch (w)
         {
             case 4: copy_tile<PACK, 16, U, NT>(s, field, buf, start, end); break;
@@ -647,7 +652,9 @@ __device__ __forceinline__ void self_pipelined(const seg_s& s, const seg_s& q,
 // cover the same buffer bytes. A workgroup packs its tile (field interior -> buffer), waits at a
 // workgroup barrier (its own stores are visible to its own waves), then unpacks the same bytes
 // (buffer -> field halo). All bytes of pack and unpack move; the hand-off never leaves the CU.
-template<int U, int NT>
+// PIPE: the software-pipelined variant (knob "self_pipe") is compiled into its own kernel, so
+// its registers (148 vs 116 VGPRs at U=4) do not cost the default kernel occupancy.
+template<int U, int NT, bool PIPE = false>
 __global__ __launch_bounds__(kBlock) void k_self(kargs a)
 {
     const seg_s* __restrict__ ps = static_cast<const seg_s*>(a.segs);
@@ -667,17 +674,20 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
         wp = min(wp, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
         int wu = min(int(q.wlog2), ptr_wlog2(reinterpret_cast<uint64_t>(field_u)));
         wu = min(wu, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
-        if (a.pipe && wp == wu && s.row_bytes < a.pipe)
+        if constexpr (PIPE)
         {
-            switch (wp)
+            if (wp == wu && s.row_bytes < a.pipe)
             {
-                case 4: self_pipelined<16, U>(s, q, field_p, field_u, buf, start, end); break;
-                case 3: self_pipelined<8, U>(s, q, field_p, field_u, buf, start, end); break;
-                case 2: self_pipelined<4, U>(s, q, field_p, field_u, buf, start, end); break;
-                case 1: self_pipelined<2, U>(s, q, field_p, field_u, buf, start, end); break;
-                default: self_pipelined<1, U>(s, q, field_p, field_u, buf, start, end); break;
+                switch (wp)
+                {
+                    case 4: self_pipelined<16, U>(s, q, field_p, field_u, buf, start, end); break;
+                    case 3: self_pipelined<8, U>(s, q, field_p, field_u, buf, start, end); break;
+                    case 2: self_pipelined<4, U>(s, q, field_p, field_u, buf, start, end); break;
+                    case 1: self_pipelined<2, U>(s, q, field_p, field_u, buf, start, end); break;
+                    default: self_pipelined<1, U>(s, q, field_p, field_u, buf, start, end); break;
+                }
+                continue;
             }
-            continue;
         }
         // Whole tile, or in chunks of a.chunk buffer bytes (g_tune.self_chunk, a knob: keeping
         // the re-read bytes in L2 this way measured no faster).
@@ -793,11 +803,16 @@ uint32_t grid_for_tiles(uint32_t n_tiles)
     return n_tiles < cap ? n_tiles : cap;
 }
 
-int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid)
+int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid, bool pairs)
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (direction == 0) launch_variant<seg_s, true>(a, s, grid);
+    // plans with paired segments (a developer knob): one variant, U = 4, default cache policy
+    if (pairs && direction == 0)
+        hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (pairs)
+        hipLaunchKernelGGL((k_copy<false, 4, 0, seg_s, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (direction == 0) launch_variant<seg_s, true>(a, s, grid);
     else launch_variant<seg_s, false>(a, s, grid);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
@@ -812,7 +827,9 @@ int launch_self(const kargs& a, void* stream, uint32_t grid)
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (g_tune.unroll == 8) hipLaunchKernelGGL((k_self<8, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+    if (a.pipe)  // software-pipelined tiles (a developer knob): one variant, U = 4
+        hipLaunchKernelGGL((k_self<4, 0, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (g_tune.unroll == 8) hipLaunchKernelGGL((k_self<8, 0>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (g_tune.unroll == 2) hipLaunchKernelGGL((k_self<2, 0>), dim3(grid), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((k_self<4, 0>), dim3(grid), dim3(kBlock), 0, s, a);
     const hipError_t e = hipGetLastError();

@@ -429,6 +429,7 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
     std::vector<uint32_t> tiles = build_tiles(segs, g_tune.pair ? &consumed : nullptr);
     n_segments = int32_t(segs.size());
     n_tiles = uint32_t(tiles.size() / 2);
+    for (const seg_s& s : segs) has_pairs = has_pairs || s.partner >= 0;
     host_segs = segs;
     upload(dev, segs, tiles);
 }
@@ -452,7 +453,7 @@ int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
         if (!bptr[i]) throw invalid("null buffer pointer");
         a.buf_ptr[i] = reinterpret_cast<uint64_t>(bptr[i]);
     }
-    return launch_structured(a, direction, stream, grid_for_tiles(n_tiles));
+    return launch_structured(a, direction, stream, grid_for_tiles(n_tiles), has_pairs);
 }
 
 // ---------------------------------------------------------------------------------------------
