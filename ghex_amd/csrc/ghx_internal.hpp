@@ -30,10 +30,11 @@ struct tuning
     int nt = 0;                     // 0 default, 1 nt stores, 2 nt loads + stores, 3 nt loads
     int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
     uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
-    uint32_t self_tile_bytes = kTileBytes;  // the same for the fused self exchange (separate
-                                       // self plans are built when it differs; with the
-                                       // barrier-free self tiles 8 KiB measured best: 4 KiB
-                                       // +0-7 %)
+    uint32_t self_tile_bytes = 4096;   // the same for the fused self exchange (separate self
+                                       // plans are built when it differs). Medians of 4
+                                       // interleaved A/B runs, lane-local k_self (116 VGPRs):
+                                       // H=2 4 KiB 28.4 vs 8 KiB 30.4 us; H=1 21.1 vs 20.5;
+                                       // H=3 41.4 vs 41.2 (profiles/r01c_self_tile_ab.jsonl)
     uint32_t small_tile_rows = 4096;   // rows per tile of segments with short rows
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
