@@ -71,11 +71,15 @@ def test_one_rank_eight_domains_two_patterns(types):
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 @pytest.mark.parametrize("layout", [(2, 1, 0), (0, 2, 1)])
 def test_fused_equals_unfused_and_oracle(Hw, layout):
-    import torch
+    fused_vs_unfused(Hw, layout, 24)
+
+
+def fused_vs_unfused(Hw, layout, N):
+    """One periodic N^3 domain: the fused self exchange and the two-launch path both write the
+    oracle's buffer bytes and fields."""
     from ghex_amd import make_context
     from ghex_amd.structured import regular as R
     from tests.gpu_util import device_field
-    N = 24
     E = N + 2 * Hw
     ranks, gf, gl = H.cube_domains(N, (1, 1, 1))
     dom = ranks[0][0]
