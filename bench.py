@@ -364,6 +364,13 @@ def main():
         t_cold = cold_duration(torch, dev, stream, dom_fn, lambda s: fl.add_(1.0))
         out["roofline"]["cold_launch_us"] = round(t_cold * 1e6, 2)
         out["roofline"]["cold_achieved"] = round(launch_bytes / t_cold / 1e9, 1)
+        # the same with a read-only flush (1 GiB reduction): caches cold but not dirty, so the
+        # launch does not also pay for writing back the flush's dirty lines it evicts
+        acc = torch.empty((), dtype=torch.float64, device=dev)
+        t_clean = cold_duration(torch, dev, stream, dom_fn,
+                                lambda s: torch.sum(fl, dim=(0,), out=acc))
+        out["roofline"]["cold_clean_launch_us"] = round(t_clean * 1e6, 2)
+        out["roofline"]["cold_clean_achieved"] = round(launch_bytes / t_clean / 1e9, 1)
         del fl
         torch.cuda.empty_cache()
 
