@@ -438,7 +438,7 @@ int ghx_tune(const char* key, int32_t value)
         }
         else if (k == "self_lane_local")
         {
-            if (value < 0 || value > 1) throw invalid("self_lane_local must be 0 or 1");
+            if (value < 0 || value > 2) throw invalid("self_lane_local must be 0, 1 or 2");
             g_tune.self_lane_local = value;
         }
         else if (k == "xcd_pair")

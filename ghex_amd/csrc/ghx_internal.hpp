@@ -30,11 +30,12 @@ struct tuning
     int nt = 0;                     // 0 default, 1 nt stores, 2 nt loads + stores, 3 nt loads
     int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
     uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
-    uint32_t self_tile_bytes = 4096;   // the same for the fused self exchange (separate self
-                                       // plans are built when it differs). Medians of 4
-                                       // interleaved A/B runs, lane-local k_self (116 VGPRs):
-                                       // H=2 4 KiB 28.4 vs 8 KiB 30.4 us; H=1 21.1 vs 20.5;
-                                       // H=3 41.4 vs 41.2 (profiles/r01c_self_tile_ab.jsonl)
+    uint32_t self_tile_bytes = kTileBytes;  // the same for the fused self exchange (separate
+                                       // self plans are built when it differs). Medians of 4
+                                       // interleaved A/B runs with register forwarding
+                                       // (self_lane_local 2): H=2 8 KiB 26.4 vs 4 KiB 27.9 us;
+                                       // H=1 18.6 vs 19.9; H=3 32.8 vs 32.0
+                                       // (profiles/r01c_fwd_tile_ab.jsonl)
     uint32_t small_tile_rows = 4096;   // rows per tile of segments with short rows
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
@@ -61,8 +62,10 @@ struct tuning
                                        // x-face halo stores overlap the next chunk's loads);
                                        // 1 short-row tiles, 2 all. Measured: H=2 within noise,
                                        // H=1 +3 %, H=3 +12 % time -> off
-    int self_lane_local = 1;           // fused self exchange without the intra-tile barrier
-                                       // when both halves use the same vector width
+    int self_lane_local = 2;           // fused self exchange without the intra-tile barrier
+                                       // when both halves use the same vector width; 2: the
+                                       // unpack half takes the packed bytes from registers
+                                       // (self_forward) instead of reading the buffer back
     int xcd_pair = 1;                  // dispatch the tiles of line-sharing short-row segment
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt

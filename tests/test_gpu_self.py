@@ -103,7 +103,9 @@ def fused_vs_unfused(Hw, layout, N):
         np.testing.assert_array_equal(buf, ob)
 
 
-@pytest.mark.parametrize("knobs", [{"self_lane_local": 0}, {"self_tile_bytes": 4096},
+@pytest.mark.parametrize("knobs", [{"self_lane_local": 0}, {"self_lane_local": 1},
+                                   {"self_lane_local": 2, "self_tile_bytes": 8192},
+                                   {"self_tile_bytes": 4096},
                                    {"self_tile_bytes": 2048, "self_lane_local": 0,
                                     "self_chunk": 1024},
                                    {"self_pipe": 1}, {"self_pipe": 2, "unroll": 2},
