@@ -135,13 +135,20 @@ def main():
     L = _ghx.lib()
     ns, nr = len(send), len(recv)
 
+    # N=2/4: a rank has self messages (its periodic wrap in the undecomposed dimensions) AND peer
+    # messages; the communication object then completes the self messages inside the pack
+    # launch and unpacks the peer messages only (ghx_exchange_pack_self / _unpack_peers)
+    mixed = co.fuse_self and co.mixed(plan) and not args.unfused
+    pack_fn = L.ghx_exchange_pack_self if mixed else L.ghx_exchange_pack
+    unpack_fn = L.ghx_exchange_unpack_peers if mixed else L.ghx_exchange_unpack
+
     def pack(s):
-        rc = L.ghx_exchange_pack(plan.h, fptr, 1, sptr, ns, s)
+        rc = pack_fn(plan.h, fptr, 1, sptr, ns, s)
         if rc:
             raise RuntimeError(L.ghx_last_error().decode())
 
     def unpack(s):
-        rc = L.ghx_exchange_unpack(plan.h, fptr, 1, rptr, nr, s)
+        rc = unpack_fn(plan.h, fptr, 1, rptr, nr, s)
         if rc:
             raise RuntimeError(L.ghx_last_error().decode())
 
@@ -243,7 +250,9 @@ def main():
             "launch": ("eager" if args.no_graph else
                        f"hipGraph of {args.steps_per_graph} steps") + ", " +
                       ("fused self-exchange: 1 launch per step (pack tile -> workgroup barrier "
-                       "-> unpack same bytes)" if use_fused else "pack launch + unpack launch"),
+                       "-> unpack same bytes)" if use_fused else
+                       "pack launch completing the self messages + unpack launch of the peer "
+                       "messages" if mixed else "pack launch + unpack launch"),
             "bytes_per_step_per_gpu": step_bytes,
             "parallelism": f"{world} rank(s), one domain per GPU",
         },
@@ -262,14 +271,19 @@ def main():
     else:
         # two launches per step: the timed region's device time split by their live differential
         # durations (graphs of M and M+1 launches)
-        launch_bytes = 2 * n_halo * 8
+        # (mixed: the pack launch also moves the self messages' unpack bytes, the unpack launch
+        # only the peer messages')
+        self_b = sum(b["size"] for b in plan.recv if b["rank"] == rank) if mixed else 0
+        pack_b, unpack_b = 2 * n_halo * 8 + 2 * self_b, 2 * n_halo * 8 - 2 * self_b
         dom_name, dom_d = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+        launch_bytes = pack_b if dom_name == "pack" else unpack_b
         dom_t = dev_step * dom_d / (t_pack + t_unpack)
-        kname = f"k_copy<{dom_name}>"
+        kname = ("k_self<pack + self messages>" if mixed and dom_name == "pack"
+                 else f"k_copy<{dom_name}>")
     achieved = launch_bytes / dom_t / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tfile):
+    if os.path.exists(tfile) and not mixed:  # (profiled: the N=1 launches)
         try:
             tj = json.load(open(tfile))
             ent = tj.get(f"N{N}_H{Hw}", {}).get(dom_name)

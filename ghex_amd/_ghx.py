@@ -89,6 +89,9 @@ _SIGS = {
     "ghx_exchange_unpack": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
     "ghx_exchange_self_fusable": (c_i32, [c_vp, P(c_i32)]),
     "ghx_exchange_self": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_exchange_mixed": (c_i32, [c_vp, P(c_i32)]),
+    "ghx_exchange_pack_self": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_exchange_unpack_peers": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
     "ghx_unstructured_pack": (c_i32, [P(UDataDesc), c_vp, c_vp, c_vp, c_i32, ctypes.c_int64, c_vp]),
     "ghx_unstructured_unpack": (c_i32, [P(UDataDesc), c_vp, c_vp, c_vp, c_i32, ctypes.c_int64, c_vp]),
     "ghx_ipc_export": (c_i32, [c_vp, P(ctypes.c_ubyte), P(ctypes.c_uint64)]),

@@ -157,6 +157,15 @@ class CommunicationObject:
             plan._all_self = bool(f.value) and all(b["rank"] == me for b in plan.send + plan.recv)
         return plan._all_self
 
+    def mixed(self, plan) -> bool:
+        """Self AND peer messages: the pack launch also completes the self messages
+        (ghx_exchange_pack_self) and the unpack launch covers the peers only."""
+        if getattr(plan, "_mixed", None) is None:
+            f = ctypes.c_int32()
+            _ghx.call("ghx_exchange_mixed", plan.h, ctypes.byref(f))
+            plan._mixed = bool(f.value)
+        return plan._mixed
+
     # -- planning -----------------------------------------------------------------------------
     def _key(self, bis):
         k = []
@@ -271,8 +280,9 @@ class CommunicationObject:
                 _ghx.call("ghx_exchange_self", plan.h, fptrs, len(bis), sptrs, len(send),
                           stream.cuda_stream)
             else:
-                _ghx.call("ghx_exchange_pack", plan.h, fptrs, len(bis), sptrs, len(send),
-                          stream.cuda_stream)
+                mixed = self.fuse_self and self.mixed(plan)
+                _ghx.call("ghx_exchange_pack_self" if mixed else "ghx_exchange_pack", plan.h,
+                          fptrs, len(bis), sptrs, len(send), stream.cuda_stream)
                 me = self.context.rank()
                 sends = [(x["rank"], x["tag"], send[i][:x["size"]])
                          for i, x in enumerate(plan.send) if x["rank"] != me]
@@ -283,8 +293,8 @@ class CommunicationObject:
                 else:
                     for w in route(self.context, sends, recvs):
                         w.wait()  # NCCL: the stream waits for the recvs, the host does not
-                _ghx.call("ghx_exchange_unpack", plan.h, fptrs, len(bis), rptrs, len(recv),
-                          stream.cuda_stream)
+                _ghx.call("ghx_exchange_unpack_peers" if mixed else "ghx_exchange_unpack",
+                          plan.h, fptrs, len(bis), rptrs, len(recv), stream.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(stream)
         return CommunicationHandle(self, stream, ev)
@@ -337,6 +347,28 @@ class CommunicationObject:
         s = (stream or torch.cuda.current_stream()).cuda_stream
         _ghx.call("ghx_exchange_pack", plan.h, _ghx.ptr_array([b.field.data_ptr() for b in bis]),
                   len(bis), _ghx.ptr_array([t.data_ptr() for t in send]), len(send), s)
+        return plan, send, recv
+
+    def pack_self_only(self, bis, stream=None):
+        """Mixed exchanges: pack every send buffer and complete the self messages."""
+        import torch
+        plan = self.plan(bis)
+        send, recv = self.buffers(plan, bis[0].field.device)
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        _ghx.call("ghx_exchange_pack_self", plan.h,
+                  _ghx.ptr_array([b.field.data_ptr() for b in bis]), len(bis),
+                  _ghx.ptr_array([t.data_ptr() for t in send]), len(send), s)
+        return plan, send, recv
+
+    def unpack_peers_only(self, bis, stream=None):
+        """Mixed exchanges: unpack the peer messages only."""
+        import torch
+        plan = self.plan(bis)
+        send, recv = self.buffers(plan, bis[0].field.device)
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        _ghx.call("ghx_exchange_unpack_peers", plan.h,
+                  _ghx.ptr_array([b.field.data_ptr() for b in bis]), len(bis),
+                  _ghx.ptr_array([t.data_ptr() for t in recv]), len(recv), s)
         return plan, send, recv
 
     def unpack_only(self, bis, stream=None):

@@ -200,6 +200,12 @@ struct exchange_plan
     // the fused self exchange's own pack/unpack plans when its tile size differs from the
     // two-launch path's (g_tune.self_tile_bytes); null = use spack/sunpack
     std::unique_ptr<splan> self_pack, self_unpack;
+    // exchanges with self AND peer messages (build_mixed): per segment of spack the unpack
+    // segment of its self message (zero = a peer message: pack only), and the unpack plan of
+    // the peer messages alone
+    device_tables mixed_comp;
+    std::unique_ptr<splan> punpack;
+    bool mixed = false;
     int32_t n_items = 0;
     mutable int self_ok = -1;  // lazily checked: may pack and unpack be fused (all self)?
 
@@ -380,6 +386,84 @@ void plan_direction(const ghx_exchange_item* items, int n_items, bool receive,
     }
 }
 
+// Exchanges with self AND peer messages — a rank whose periodic wrap reaches itself next to real
+// neighbours, e.g. the (2,1,1) and (2,2,1) decompositions: the pack launch also writes the halos
+// of the self messages straight from the registers it packs them from (k_self's forwarding path),
+// and the unpack launch covers the peer messages only. Companion segment k of the pack plan is
+// the unpack segment of the same buffer bytes for a self message (same tiling, checked), or
+// zero for a peer message. `rent` = the receive-side pack entries of every recv buffer.
+void build_mixed(exchange_plan& ex, int32_t me, const std::vector<ghx_pack_entry>& rent)
+{
+    if (!ex.spack || !ex.sunpack || ex.upack || ex.uunpack || me < 0 || ex.self_fusable()) return;
+    std::vector<int> send_of_recv(ex.recv.size(), -1);
+    bool any_self = false;
+    for (size_t j = 0; j < ex.recv.size(); ++j)
+    {
+        const xbuffer& r = ex.recv[j];
+        if (r.rank != me) continue;
+        for (size_t i = 0; i < ex.send.size(); ++i)
+        {
+            const xbuffer& s = ex.send[i];
+            if (s.rank == me && s.first_id == r.first_id && s.second_id == r.second_id &&
+                s.size == r.size)
+            {
+                send_of_recv[j] = int(i);
+                any_self = true;
+                break;
+            }
+        }
+    }
+    if (!any_self) return;
+    std::vector<ghx_pack_entry> self_e, peer_e;
+    for (const ghx_pack_entry& e : rent)
+    {
+        const int i = send_of_recv[size_t(e.buffer_slot)];
+        if (i < 0)
+        {
+            peer_e.push_back(e);
+            continue;
+        }
+        ghx_pack_entry s = e;
+        s.buffer_slot = i;  // a self message's recv buffer IS its send buffer
+        self_e.push_back(s);
+    }
+    if (peer_e.empty()) return;
+    std::stable_sort(self_e.begin(), self_e.end(),
+                     [](const ghx_pack_entry& a, const ghx_pack_entry& b) {
+                         return a.buffer_slot < b.buffer_slot;
+                     });
+    const splan su(self_e.data(), int(self_e.size()), 1);
+    std::vector<char> is_self(ex.send.size(), 0);
+    for (int i : send_of_recv)
+        if (i >= 0) is_self[size_t(i)] = 1;
+    const std::vector<seg_s>& ps = ex.spack->host_segs;
+    std::vector<seg_s> comp(ps.size());  // value-initialised: bytes = 0 -> pack only
+    size_t m = 0;
+    bool short_self = false;
+    for (size_t k = 0; k < ps.size(); ++k)
+    {
+        if (!is_self[ps[k].buf_slot]) continue;
+        short_self = short_self || ps[k].row_bytes < g_tune.small_row_bytes;
+        if (m >= su.host_segs.size()) return;
+        const seg_s& q = su.host_segs[m++];
+        if (q.buf_slot != ps[k].buf_slot || q.buf_off != ps[k].buf_off || q.bytes != ps[k].bytes ||
+            q.row_bytes != ps[k].row_bytes || q.tile_bytes != ps[k].tile_bytes ||
+            ps[k].partner >= 0 || q.bytes == 0)
+            return;
+        comp[k] = q;
+    }
+    if (m != su.host_segs.size()) return;
+    // Worth it only when the self messages include request-bound short rows (the unit-stride
+    // x-faces of an x-local decomposition such as (1,1,2)): fusing their reads and writes into
+    // one launch is what the fused self exchange gains. Self messages of long rows alone (the
+    // y/z wrap of a (2,1,1) decomposition) measured 1-3 % slower mixed than plain
+    // (tools/emu_rank_bench.py, profiles/r01c_emu_rank.jsonl).
+    if (!short_self && !g_tune.mixed_always) return;
+    upload_segments(ex.mixed_comp, comp);
+    ex.punpack = std::make_unique<splan>(peer_e.data(), int(peer_e.size()), 1);
+    ex.mixed = true;
+}
+
 int check_ptr(const void* p, const char* what)
 {
     if (!p) throw invalid(std::string("null argument: ") + what);
@@ -440,6 +524,11 @@ int ghx_tune(const char* key, int32_t value)
         {
             if (value < 0 || value > 2) throw invalid("self_lane_local must be 0, 1 or 2");
             g_tune.self_lane_local = value;
+        }
+        else if (k == "mixed_always")
+        {
+            if (value < 0 || value > 1) throw invalid("mixed_always must be 0 or 1");
+            g_tune.mixed_always = value;
         }
         else if (k == "xcd_pair")
         {
@@ -847,6 +936,8 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
         if (n_items > GHX_MAX_SLOTS) throw invalid("at most 64 fields per exchange");
         auto ex = std::make_unique<ghx_exchange>();
         ex->n_items = n_items;
+        std::vector<ghx_pack_entry> rent;              // receive entries, for build_mixed
+        std::vector<std::vector<ghx_box>> rstore;      // (their boxes)
         for (int dir = 0; dir < 2; ++dir)
         {
             const bool receive = dir == 1;
@@ -856,6 +947,11 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
             store.reserve(size_t(n_items) * 64);
             auto& bufs = receive ? ex->recv : ex->send;
             plan_direction(items, n_items, receive, bufs, sent, uent, store);
+            if (receive)
+            {
+                rent = sent;
+                rstore = std::move(store);  // moves the inner vectors: box pointers stay valid
+            }
             if (bufs.size() > GHX_MAX_SLOTS) throw invalid("more than 64 peer buffers");
             if (!sent.empty())
                 (receive ? ex->sunpack : ex->spack) =
@@ -887,6 +983,7 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
             ex->self_pack.reset();
             ex->self_unpack.reset();
         }
+        build_mixed(*ex, items[0].pattern->my_rank, rent);
         *out = ex.release();
         return GHX_OK;
     });
@@ -998,6 +1095,60 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
             a.buf_ptr[i] = reinterpret_cast<uint64_t>(buffers[i]);
         }
         return launch_self(a, stream, grid_for_tiles(p.n_tiles));
+    });
+}
+
+int ghx_exchange_mixed(const ghx_exchange* ex, int32_t* mixed)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        check_ptr(mixed, "mixed");
+        *mixed = ex->mixed ? 1 : 0;
+        return GHX_OK;
+    });
+}
+
+int ghx_exchange_pack_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                           void* const* send_buffers, int32_t n_send, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        if (!ex->mixed) throw invalid("exchange has no mixed self/peer plan (ghx_exchange_mixed)");
+        const splan& p = *ex->spack;
+        if (n_send < int32_t(ex->send.size())) throw invalid("too few send buffers");
+        if (n_fields <= p.max_field_slot || n_send <= p.max_buf_slot)
+            throw invalid("pointer arrays do not cover the plan's slots");
+        if (!p.dev.segs || !ex->mixed_comp.segs) throw hip_error("plan has no device tables");
+        kargs a{};
+        a.segs = p.dev.segs;
+        a.segs2 = ex->mixed_comp.segs;
+        a.chunk = g_tune.self_chunk;
+        a.lane_local = uint32_t(g_tune.self_lane_local);
+        a.pipe = 0;
+        a.tile_seg = p.dev.tiles;
+        a.n_tiles = p.n_tiles;
+        for (int i = 0; i <= p.max_field_slot; ++i)
+        {
+            if (!field_ptrs[i]) throw invalid("null field pointer");
+            a.field_ptr[i] = reinterpret_cast<uint64_t>(field_ptrs[i]);
+        }
+        for (int i = 0; i <= p.max_buf_slot; ++i)
+        {
+            if (!send_buffers[i]) throw invalid("null buffer pointer");
+            a.buf_ptr[i] = reinterpret_cast<uint64_t>(send_buffers[i]);
+        }
+        return launch_self(a, stream, grid_for_tiles(p.n_tiles));
+    });
+}
+
+int ghx_exchange_unpack_peers(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                              void* const* recv_buffers, int32_t n_recv, ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        if (!ex->mixed) throw invalid("exchange has no mixed self/peer plan (ghx_exchange_mixed)");
+        if (n_recv < int32_t(ex->recv.size())) throw invalid("too few recv buffers");
+        return ex->punpack->execute(field_ptrs, n_fields, recv_buffers, n_recv, stream);
     });
 }
 

@@ -70,6 +70,8 @@ struct tuning
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt
                                        // round-robin over the 8 XCDs) at the same time
+    int mixed_always = 0;              // build the mixed self/peer plans even when the self
+                                       // messages hold no short rows (tests, measurements)
 };
 extern tuning g_tune;
 

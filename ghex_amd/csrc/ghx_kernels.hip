@@ -722,6 +722,12 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
         wp = min(wp, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
         int wu = min(int(q.wlog2), ptr_wlog2(reinterpret_cast<uint64_t>(field_u)));
         wu = min(wu, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+        if (q.bytes == 0)
+        {
+            // a peer message of a mixed exchange (ghx_exchange_pack_self): pack only
+            copy_any<true, U, NT>(s, field_p, buf, start, end, wp);
+            continue;
+        }
         if constexpr (PIPE)
         {
             if (wp == wu && s.row_bytes < a.pipe)

@@ -164,6 +164,7 @@ int regular_make_pattern(int dim, const ghx_regular_domain* doms, int n, const i
     out.kind = 0;
     out.dim = dim;
     out.max_tag = max_tag;
+    out.my_rank = my_rank;
     if (my_rank < 0 || my_rank >= world) return GHX_OK;
     for (int a : by_rank[my_rank])
     {
@@ -306,6 +307,7 @@ int unstructured_make_pattern(int n, const int32_t* ids, const int32_t* ranks,
     out.kind = 1;
     out.dim = 1;
     out.max_tag = make_tag(max_num_domains, max_domain_id);
+    out.my_rank = my_rank;
     if (my_rank >= world) return GHX_OK;
     for (size_t li = 0; li < by_rank[my_rank].size(); ++li)
     {

@@ -45,6 +45,7 @@ struct pattern_set
     int kind = 0;  // 0 structured, 1 unstructured
     int dim = 3;
     int32_t max_tag = 0;
+    int32_t my_rank = -1;  // the rank the pattern was made for (self messages: remote_rank ==)
     std::vector<domain_pattern> doms;
 };
 

@@ -258,6 +258,16 @@ void device_tables::release()
     lids = nullptr;
 }
 
+void upload_segments(device_tables& dt, const std::vector<seg_s>& segs)
+{
+    dt.release();
+    if (segs.empty() || !have_device()) return;
+    const size_t sb = segs.size() * sizeof(seg_s);
+    if (hipMalloc(&dt.segs, sb) != hipSuccess) throw hip_error("hipMalloc(segments)");
+    if (hipMemcpy(dt.segs, segs.data(), sb, hipMemcpyHostToDevice) != hipSuccess)
+        throw hip_error("hipMemcpy(segments)");
+}
+
 // ---------------------------------------------------------------------------------------------
 // structured
 // ---------------------------------------------------------------------------------------------

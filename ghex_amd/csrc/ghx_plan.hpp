@@ -31,6 +31,8 @@ struct device_tables
 };
 
 void validate_field(const ghx_field_desc& f);
+// segment table alone to device memory (a no-op without a HIP device)
+void upload_segments(device_tables& dt, const std::vector<seg_s>& segs);
 uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, const ghx_box& box,
                           uint16_t field_slot, uint16_t buf_slot, uint64_t buf_off);
 

@@ -297,12 +297,25 @@ int ghx_exchange_unpack(const ghx_exchange* ex, void* const* field_ptrs, int32_t
  * the device in the reference's stream-aware flow either (communication_object.hpp:703-767:
  * pack -> send to self -> unpack). When EVERY message of an exchange is a self message
  * (*fusable = 1), ghx_exchange_self performs pack and unpack in ONE launch: each workgroup packs
- * a tile of the send buffer and then unpacks the same bytes into the halos (workgroup barrier in
- * between). The buffers are the send buffers (they double as recv buffers); every byte of both
- * pack and unpack is moved, and the send buffers hold the packed message afterwards. */
+ * a tile of the send buffer and then writes the same bytes into the halos (from the registers it
+ * stored them from, or after a workgroup barrier). The buffers are the send buffers (they double
+ * as recv buffers); every packed byte and every halo byte is written, and the send buffers hold
+ * the packed message afterwards. */
 int ghx_exchange_self_fusable(const ghx_exchange* ex, int32_t* fusable);
 int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
                       void* const* buffers, int32_t n_buffers, ghx_stream stream);
+
+/* Exchanges with self messages AND peer messages (*mixed = 1; e.g. a (2,1,1) periodic
+ * decomposition: x to the neighbour, y and z onto the rank itself): ghx_exchange_pack_self packs
+ * every send buffer AND completes the self messages (their halos written in the same launch);
+ * the transport then carries the peer messages only, and ghx_exchange_unpack_peers unpacks the
+ * peer recv buffers only (same pointer arrays as ghx_exchange_pack/unpack). Together they do
+ * exactly what ghx_exchange_pack + ghx_exchange_unpack do. */
+int ghx_exchange_mixed(const ghx_exchange* ex, int32_t* mixed);
+int ghx_exchange_pack_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                           void* const* send_buffers, int32_t n_send, ghx_stream stream);
+int ghx_exchange_unpack_peers(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
+                              void* const* recv_buffers, int32_t n_recv, ghx_stream stream);
 
 /* ------------------------------------------------------------------------------------------
  * Zero-copy put between node-local GPUs. Replaces the reference's RMA path:

@@ -42,15 +42,19 @@ class FakeContext:
         return r
 
 
-def emulated_exchange(cos, bis_per_rank):
+def emulated_exchange(cos, bis_per_rank, mixed=False):
     """Pack on every emulated rank, route send buffers to the matching recv buffers by
-    (sender rank, domain pair, tag), unpack on every rank (all on one stream)."""
+    (sender rank, domain pair, tag), unpack on every rank (all on one stream). mixed=True: the
+    product's path for exchanges with self AND peer messages (ghx_exchange_pack_self, then
+    ghx_exchange_unpack_peers) on every rank whose plan has one."""
     import torch
-    plans, bufs = [], []
+    plans, bufs, used = [], [], []
     for r, (co, bis) in enumerate(zip(cos, bis_per_rank)):
-        plan, send, recv = co.pack_only(bis)
+        m = mixed and co.mixed(co.plan(bis))
+        plan, send, recv = co.pack_self_only(bis) if m else co.pack_only(bis)
         plans.append(plan)
         bufs.append((send, recv))
+        used.append(m)
     for r, plan in enumerate(plans):
         send_r, recv_r = bufs[r]
         for i, x in enumerate(plan.recv):
@@ -62,7 +66,12 @@ def emulated_exchange(cos, bis_per_rank):
             assert plans[src].send[j]["tag"] == x["tag"]
             assert plans[src].send[j]["size"] == x["size"]
             recv_r[i][:x["size"]].copy_(bufs[src][0][j][:x["size"]])
-    for co, bis in zip(cos, bis_per_rank):
-        co.unpack_only(bis)
+    for co, bis, m in zip(cos, bis_per_rank, used):
+        if m:
+            co.unpack_peers_only(bis)
+        else:
+            co.unpack_only(bis)
     torch.cuda.synchronize()
+    if mixed:
+        emulated_exchange.mixed_ranks = sum(used)
     return plans, bufs

@@ -103,11 +103,14 @@ def test_dtypes_exchange(dtype):
                                   .cpu().numpy(), ob)
 
 
+@pytest.mark.parametrize("mixed", [False, True])
 @pytest.mark.parametrize("types", [(np.float64, np.float32, np.int32),
                                    (np.float64, np.float64, np.float64)])
-def test_reference_geometry_4ranks_emulated(types):
+def test_reference_geometry_4ranks_emulated(types, mixed):
     """test_regular_domain.cpp: 4 ranks x 2 domains, 3 fields of array<T,3>, 2 patterns;
-    emulated in one process on one GPU; every byte vs the oracle exchange."""
+    emulated in one process on one GPU; every byte vs the oracle exchange. mixed: the messages
+    between a rank's own two domains are completed in the pack launch (ghx_exchange_pack_self)
+    and only the peer messages unpacked."""
     import torch
     from ghex_amd.structured import regular as R
     from tests.gpu_util import FakeContext, device_field, emulated_exchange
@@ -140,7 +143,14 @@ def test_reference_geometry_4ranks_emulated(types):
         cos.append(R.make_communication_object(ctx))
         bis_all.append(bis)
     obufs = orc.regular_exchange(ranks_fields, pat_o, 4)
-    plans, bufs = emulated_exchange(cos, bis_all)
+    from ghex_amd import _ghx
+    _ghx.call("ghx_tune", b"mixed_always", 1 if mixed else 0)
+    try:
+        plans, bufs = emulated_exchange(cos, bis_all, mixed=mixed)
+    finally:
+        _ghx.call("ghx_tune", b"reset", 0)
+    if mixed:
+        assert emulated_exchange.mixed_ranks > 0
     for b, a in zip(bases, oracle_arrays):
         np.testing.assert_array_equal(b.cpu().numpy(), a)
     # byte parity of every send buffer (pads masked)
@@ -175,8 +185,25 @@ def _as_struct_elem(fd, elem):
     return fd
 
 
+@pytest.mark.parametrize("parts,always", [((1, 1, 2), 0), ((1, 2, 2), 0), ((1, 2, 1), 0),
+                                          ((2, 1, 1), 1), ((2, 2, 1), 1)])
+def test_cube_multi_rank_emulated_mixed(parts, always):
+    """Decompositions whose ranks have self AND peer messages: the pack launch completes the
+    self messages (register forwarding), the unpack launch only the peer ones. x-local
+    decompositions get the mixed plans by default (their self messages hold the short x rows);
+    for (2,1,1) / (2,2,1) they are forced with the knob mixed_always."""
+    from ghex_amd import _ghx
+    from tests.gpu_util import emulated_exchange
+    _ghx.call("ghx_tune", b"mixed_always", always)
+    try:
+        test_cube_multi_rank_emulated(parts, mixed=True)
+    finally:
+        _ghx.call("ghx_tune", b"reset", 0)
+    assert emulated_exchange.mixed_ranks == parts[0] * parts[1] * parts[2]
+
+
 @pytest.mark.parametrize("parts", [(2, 1, 1), (2, 2, 2), (3, 2, 1)])
-def test_cube_multi_rank_emulated(parts):
+def test_cube_multi_rank_emulated(parts, mixed=False):
     from ghex_amd.structured import regular as R
     from tests.gpu_util import FakeContext, device_field, emulated_exchange
     N, Hw = 10, 2
@@ -198,7 +225,7 @@ def test_cube_multi_rank_emulated(parts):
         arrs.append(a)
         rf.append([(spec, ranks[r][0].id, 0, 0)])
     orc.regular_exchange(rf, {0: opat}, nr)
-    emulated_exchange(cos, bis)
+    emulated_exchange(cos, bis, mixed=mixed)
     for b, a, doms in zip(bases, arrs, ranks):
         np.testing.assert_array_equal(b.cpu().numpy(), a)
         np.testing.assert_array_equal(a, H.expected_linear_halo(a, doms[0], N, Hw, gl))
