@@ -330,6 +330,7 @@ class communication_object
         ghx_exchange* ex = nullptr;
         std::vector<buf> send, recv;
         bool fused = false;
+        bool mixed = false;  // self AND peer messages: ghx_exchange_pack_self / _unpack_peers
         std::vector<void*> sptr, rptr;
         ~plan()
         {
@@ -545,6 +546,9 @@ class communication_object
         std::int32_t fusable = 0;
         check_ghx(ghx_exchange_self_fusable(p->ex, &fusable), "ghx_exchange_self_fusable");
         p->fused = m_opt.fuse_self && all_self && fusable;
+        std::int32_t mixed = 0;
+        check_ghx(ghx_exchange_mixed(p->ex, &mixed), "ghx_exchange_mixed");
+        p->mixed = m_opt.fuse_self && !m_opt.self_through_transport && !p->fused && mixed;
         for (auto& b : p->send) p->sptr.push_back(b.data);
         for (auto& b : p->recv) p->rptr.push_back(b.data);
         auto& ref = *p;
@@ -569,7 +573,12 @@ class communication_object
             check_ghx(ghx_exchange_self(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream), "ghx_exchange_self");
         else
         {
-            check_ghx(ghx_exchange_pack(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream), "ghx_exchange_pack");
+            if (p.mixed)  // the pack launch also completes the self messages
+                check_ghx(ghx_exchange_pack_self(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream),
+                          "ghx_exchange_pack_self");
+            else
+                check_ghx(ghx_exchange_pack(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream),
+                          "ghx_exchange_pack");
             const int me = m_ctx->rank();
             std::vector<message> sends, recvs;
             for (auto& b : p.send)
@@ -577,7 +586,12 @@ class communication_object
             for (auto& b : p.recv)
                 if (b.rank != me || m_opt.self_through_transport) recvs.push_back({b.data, b.size, b.rank, b.tag});
             if (!sends.empty() || !recvs.empty()) m_ctx->get_transport().exchange(sends, recvs, m_stream);
-            check_ghx(ghx_exchange_unpack(p.ex, fptrs.data(), nf, p.rptr.data(), nr, m_stream), "ghx_exchange_unpack");
+            if (p.mixed)
+                check_ghx(ghx_exchange_unpack_peers(p.ex, fptrs.data(), nf, p.rptr.data(), nr, m_stream),
+                          "ghx_exchange_unpack_peers");
+            else
+                check_ghx(ghx_exchange_unpack(p.ex, fptrs.data(), nf, p.rptr.data(), nr, m_stream),
+                          "ghx_exchange_unpack");
         }
         check_hip(hipEventRecord(m_done, m_stream), "hipEventRecord");
         m_valid = true;

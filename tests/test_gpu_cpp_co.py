@@ -65,7 +65,9 @@ def test_co_loopback_all_gather_cpu(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("parts,N,H", [((1, 1, 1), 12, 2), ((2, 1, 1), 10, 2),
                                        ((2, 2, 1), 9, 1), ((2, 2, 2), 8, 3),
-                                       ((3, 1, 2), 7, 2)])
+                                       ((3, 1, 2), 7, 2),
+                                       # x-local: self messages hold the x rows -> mixed plans
+                                       ((1, 1, 2), 10, 2), ((1, 2, 2), 9, 3)])
 def test_co_loopback_structured(parts, N, H):
     """PX*PY*PZ ranks (threads) each with one N^3 domain and a double + a float field in one
     exchange (mixed alignment pads), two exchanges (plan reuse); every cell of every rank."""
