@@ -270,31 +270,43 @@ class CommunicationObject:
         device = bis[0].field.device
         plan = self.plan(bis)
         send, recv = self.buffers(plan, device)
-        fptrs = _ghx.ptr_array([bi.field.data_ptr() for bi in bis])
-        sptrs = _ghx.ptr_array([t.data_ptr() for t in send])
-        rptrs = _ghx.ptr_array([t.data_ptr() for t in recv])
+        # pointer arrays cached per (plan, field pointers): repeated exchanges of the same fields
+        # (the common case) rebuild nothing on the host
+        fkey = tuple(bi.field.data_ptr() for bi in bis)
+        cache = plan.__dict__.setdefault("_ptr_cache", {})
+        arrs = cache.get(fkey)
+        if arrs is None:
+            if len(cache) > 64:
+                cache.clear()
+            arrs = cache[fkey] = (_ghx.ptr_array(list(fkey)),
+                                  _ghx.ptr_array([t.data_ptr() for t in send]),
+                                  _ghx.ptr_array([t.data_ptr() for t in recv]))
+        fptrs, sptrs, rptrs = arrs
         self._valid = True
+        if self.fuse_self and self.all_self(plan):
+            # every message stays on this device: pack + unpack in one launch (the launch and
+            # the event go to `stream` explicitly: no current-stream switch needed)
+            _ghx.call("ghx_exchange_self", plan.h, fptrs, len(bis), sptrs, len(send),
+                      stream.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            return CommunicationHandle(self, stream, ev)
         with torch.cuda.stream(stream):
-            if self.fuse_self and self.all_self(plan):
-                # every message stays on this device: pack + unpack in one launch
-                _ghx.call("ghx_exchange_self", plan.h, fptrs, len(bis), sptrs, len(send),
-                          stream.cuda_stream)
+            mixed = self.fuse_self and self.mixed(plan)
+            _ghx.call("ghx_exchange_pack_self" if mixed else "ghx_exchange_pack", plan.h,
+                      fptrs, len(bis), sptrs, len(send), stream.cuda_stream)
+            me = self.context.rank()
+            sends = [(x["rank"], x["tag"], send[i][:x["size"]])
+                     for i, x in enumerate(plan.send) if x["rank"] != me]
+            recvs = [(x["rank"], x["tag"], recv[i][:x["size"]])
+                     for i, x in enumerate(plan.recv) if x["rank"] != me]
+            if self.staging == "host":
+                self._exchange_host_staged(plan, sends, recvs, stream)
             else:
-                mixed = self.fuse_self and self.mixed(plan)
-                _ghx.call("ghx_exchange_pack_self" if mixed else "ghx_exchange_pack", plan.h,
-                          fptrs, len(bis), sptrs, len(send), stream.cuda_stream)
-                me = self.context.rank()
-                sends = [(x["rank"], x["tag"], send[i][:x["size"]])
-                         for i, x in enumerate(plan.send) if x["rank"] != me]
-                recvs = [(x["rank"], x["tag"], recv[i][:x["size"]])
-                         for i, x in enumerate(plan.recv) if x["rank"] != me]
-                if self.staging == "host":
-                    self._exchange_host_staged(plan, sends, recvs, stream)
-                else:
-                    for w in route(self.context, sends, recvs):
-                        w.wait()  # NCCL: the stream waits for the recvs, the host does not
-                _ghx.call("ghx_exchange_unpack_peers" if mixed else "ghx_exchange_unpack",
-                          plan.h, fptrs, len(bis), rptrs, len(recv), stream.cuda_stream)
+                for w in route(self.context, sends, recvs):
+                    w.wait()  # NCCL: the stream waits for the recvs, the host does not
+            _ghx.call("ghx_exchange_unpack_peers" if mixed else "ghx_exchange_unpack",
+                      plan.h, fptrs, len(bis), rptrs, len(recv), stream.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(stream)
         return CommunicationHandle(self, stream, ev)
