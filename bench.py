@@ -249,8 +249,8 @@ def main():
             "N": N, "halo": Hw, "fields": 1, "decomposition": list(parts),
             "launch": ("eager" if args.no_graph else
                        f"hipGraph of {args.steps_per_graph} steps") + ", " +
-                      ("fused self-exchange: 1 launch per step (pack tile -> workgroup barrier "
-                       "-> unpack same bytes)" if use_fused else
+                      ("fused self-exchange: 1 launch per step (each lane packs its buffer bytes "
+                       "and writes the halos from the same registers)" if use_fused else
                        "pack launch completing the self messages + unpack launch of the peer "
                        "messages" if mixed else "pack launch + unpack launch"),
             "bytes_per_step_per_gpu": step_bytes,

@@ -68,6 +68,9 @@ def main(rn):
             pmc[f"N512_H{h}"] = r
             traffic[f"N512_H{h}"] = {k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"]}
                                      for k, v in r.items()}
+    if not pmc:  # kernel-trace-only round (SKIP_PMC=1): keep the last PMC summary
+        print("collected", rn, "(no PMC passes)")
+        return
     with open(os.path.join(dst, f"{rn}_pmc.json"), "w") as fh:
         json.dump(pmc, fh, indent=1)
     traffic["source"] = f"profiles/{rn}_pmc.json (rocprofv3 --pmc, tools/pmc.sh)"
