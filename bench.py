@@ -59,6 +59,10 @@ def parse():
                         "always on at N=1 (self puts)")
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the nccl process group even at world size 1 (path test)")
+    p.add_argument("--rehearse", action="store_true",
+                   help="developer: N>1 ranks all on cuda:0 (RCCL refuses two ranks per GPU), "
+                        "gloo group and the host-staged transport — exercises the N>1 code path "
+                        "on a one-GPU box; its numbers are not the metric")
     return p.parse_args()
 
 
@@ -73,11 +77,28 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    if args.rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     distributed = world > 1 or args.force_dist
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if args.rehearse:
+            dist.barrier()
+        else:
+            dist.barrier(device_ids=[local])
+
+    def all_reduce_host(x, op):
+        """Reduce one python number over ranks (device tensor on nccl, host tensor on gloo)."""
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if args.rehearse else dev)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
 
     import ghex_amd
     from ghex_amd import _ghx
@@ -107,7 +128,7 @@ def main():
         ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)))
     logical = base.permute(2, 1, 0)  # (x, y, z), x contiguous: layout_map<2,1,0>
     fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (E,) * 3)
-    co = R.make_communication_object(ctx)
+    co = R.make_communication_object(ctx, staging="host" if args.rehearse else None)
     bis = [pc(fd)]
 
     # ---- verified full exchange (pack -> RCCL -> unpack) --------------------------------------
@@ -119,9 +140,7 @@ def main():
     del expect
     verified = bad == 0
     if distributed:
-        t = torch.tensor([bad], device=dev)
-        dist.all_reduce(t)
-        verified = int(t.item()) == 0
+        verified = all_reduce_host(bad, dist.ReduceOp.SUM) == 0
 
     plan = co.plan(bis)
     send, recv = co.buffers(plan, dev)
@@ -212,7 +231,7 @@ def main():
         """Host wall time of k calls (barrier + synchronize on both sides, max over ranks); with
         events=True also the device time of the region from HIP events on the launch stream."""
         if distributed:
-            dist.barrier(device_ids=[local])
+            barrier()
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
@@ -224,12 +243,10 @@ def main():
         if events:
             dev_time["s"] = e0.elapsed_time(e1) * 1e-3
         if distributed:
-            dist.barrier(device_ids=[local])
+            barrier()
         dt = time.perf_counter() - t0
         if distributed:
-            tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            dt = float(tt.item())
+            dt = all_reduce_host(dt, dist.ReduceOp.MAX)
         return dt
 
     K = args.steps
@@ -258,6 +275,9 @@ def main():
         },
         "verified": verified,
     }
+    if args.rehearse:
+        out["rehearsal"] = ("all ranks on cuda:0, gloo + host-staged transport: code-path check, "
+                            "not the metric")
 
     # ---- per-kernel HIP-event durations (dominant kernel roofline) ----------------------------
     # Differential method (removes the fixed cost of the events themselves): hipGraphs of M steps,
@@ -420,7 +440,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:
-        dist.barrier(device_ids=[local])
+        barrier()
         dist.destroy_process_group()
 
 
