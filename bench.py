@@ -313,6 +313,11 @@ def main():
     out["roofline"] = {"bound": "hbm", "kernel": kname,
                        "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                       "traffic_source": (None if traffic is None else
+                                          "profiles/pmc_traffic.json: rocprofv3 --pmc of the "
+                                          f"N=1 {dom_name} launch of the same bytes" +
+                                          ("" if world == 1 else
+                                           " (one-domain plan; per-peer buffers at N>1)")),
                        "algorithmic_bytes_per_launch": launch_bytes,
                        "launch_us": round(dom_t * 1e6, 2),
                        "launch_us_source": "HIP events on the launch stream around the timed "
