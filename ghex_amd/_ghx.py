@@ -68,6 +68,8 @@ _SIGS = {
                                        P(c_i32), P(Box), P(Box), c_i32, P(c_i32)]),
     "ghx_regular_pattern_create": (c_i32, [c_i32, P(RegularDomain), c_i32, P(c_i32), P(c_i32),
                                            P(c_i32), P(c_i32), c_i32, P(c_vp)]),
+    "ghx_staged_pattern_create": (c_i32, [c_i32, P(RegularDomain), c_i32, P(c_i32), P(c_i32),
+                                          P(c_i32), P(c_i32), P(c_i32), c_i32, P(c_vp)]),
     "ghx_unstructured_pattern_create": (c_i32, [c_i32, P(c_i32), P(c_i32), P(c_i64), P(c_i64),
                                                 P(c_i64), P(c_i64), P(c_i64), P(c_i64), c_i32,
                                                 P(c_vp)]),

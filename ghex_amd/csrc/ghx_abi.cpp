@@ -780,6 +780,42 @@ int ghx_regular_pattern_create(int32_t dim, const ghx_regular_domain* domains,
     });
 }
 
+int ghx_staged_pattern_create(int32_t dim, const ghx_regular_domain* domains, int32_t n_domains,
+                              const int32_t* neighbors, const int32_t* global_first,
+                              const int32_t* global_last, const int32_t* halos,
+                              const int32_t* periodic, int32_t my_rank, ghx_pattern** out)
+{
+    return guarded([&] {
+        check_ptr(out, "out");
+        check_ptr(domains, "domains");
+        check_ptr(neighbors, "neighbors");
+        check_ptr(global_first, "global_first");
+        check_ptr(global_last, "global_last");
+        check_ptr(halos, "halos");
+        check_ptr(periodic, "periodic");
+        if (dim < 1 || dim > 3) throw invalid("dim must be 1, 2 or 3");
+        if (n_domains < 1) throw invalid("need at least one domain");
+        std::vector<ghx::pattern_set> sets;
+        try
+        {
+            ghx::staged_make_pattern(dim, domains, n_domains, neighbors, global_first,
+                                     global_last, halos, periodic, my_rank, sets);
+        }
+        catch (const std::runtime_error& e)
+        {
+            throw invalid(e.what());
+        }
+        std::vector<std::unique_ptr<ghx_pattern>> ps;
+        for (auto& s : sets)
+        {
+            ps.push_back(std::make_unique<ghx_pattern>());
+            static_cast<ghx::pattern_set&>(*ps.back()) = std::move(s);
+        }
+        for (int i = 0; i < dim; ++i) out[i] = ps[i].release();
+        return GHX_OK;
+    });
+}
+
 int ghx_unstructured_pattern_create(int32_t n_domains, const int32_t* domain_ids,
                                     const int32_t* domain_ranks, const int64_t* gids,
                                     const int64_t* gid_counts, const int64_t* outer_lids,

@@ -347,4 +347,149 @@ int unstructured_make_pattern(int n, const int32_t* ids, const int32_t* ranks,
     }
     return GHX_OK;
 }
+// ---------------------------------------------------------------------------------------------
+// staged (dimension-by-dimension) patterns
+// ---------------------------------------------------------------------------------------------
+// make_staged_pattern (include/ghex/structured/regular/make_pattern.hpp:47-250): one pattern per
+// dimension. Stage i exchanges the two halo slabs of dimension i only, over the domain box
+// already extended by the halos of the stages before it, so that running the stages in order
+// fills edges and corners without diagonal messages. Keys hold the neighbour the user's domain
+// lookup names (nbrs: per domain and dimension the left and right neighbour's id); tags are
+// assigned by the receivers per remote rank over their patterns in order (make_pattern.hpp:
+// 199-243), max_tag is the receiving rank's own maximum (make_pattern.hpp:201, 227).
+void staged_make_pattern(int dim, const ghx_regular_domain* doms, int n, const int32_t* nbrs,
+                         const int32_t* gfirst, const int32_t* glast, const int32_t* halos,
+                         const int32_t* periodic, int my_rank, std::vector<pattern_set>& out)
+{
+    if (dim < 1 || dim > 3 || n < 1) throw std::runtime_error("staged pattern: bad dim / count");
+    std::map<int32_t, int> index_of;
+    int world = 0;
+    for (int a = 0; a < n; ++a)
+    {
+        if (doms[a].rank < 0) throw std::runtime_error("staged pattern: negative rank");
+        if (!index_of.emplace(doms[a].id, a).second)
+            throw std::runtime_error("staged pattern: domain ids must be unique");
+        world = std::max(world, doms[a].rank + 1);
+    }
+    auto neighbour = [&](int a, int i, int side) -> int {
+        const int32_t id = nbrs[(a * dim + i) * 2 + side];
+        auto it = index_of.find(id);
+        if (it == index_of.end())
+            throw std::runtime_error("staged pattern: the domain lookup names an unknown neighbour");
+        return it->second;
+    };
+    using keyed = std::map<int32_t, std::vector<is_pair>>;  // remote id -> spaces (map order)
+    std::vector<std::vector<keyed>> recv(dim, std::vector<keyed>(n)), send(dim, std::vector<keyed>(n));
+    for (int a = 0; a < n; ++a)
+    {
+        is_pair ext{};
+        for (int c = 0; c < dim; ++c)
+        {
+            ext.lf[c] = 0;
+            ext.ll[c] = doms[a].last[c] - doms[a].first[c];
+            ext.gf[c] = doms[a].first[c];
+            ext.gl[c] = doms[a].last[c];
+        }
+        for (int i = 0; i < dim; ++i)
+        {
+            const int hl = halos[2 * i], hr = halos[2 * i + 1];
+            const bool has_left = hl > 0 && (periodic[i] || ext.gf[i] - hl >= gfirst[i]);
+            const bool has_right = hr > 0 && (periodic[i] || ext.gl[i] + hr <= glast[i]);
+            const int32_t left = has_left ? doms[neighbour(a, i, 0)].id : -1;
+            const int32_t right = has_right ? doms[neighbour(a, i, 1)].id : -1;
+            if (has_left)
+            {
+                is_pair x = ext;  // recv_left
+                x.ll[i] = x.lf[i] - 1;
+                x.lf[i] -= hl;
+                x.gl[i] = x.gf[i] - 1;
+                x.gf[i] -= hl;
+                recv[i][a][left].push_back(x);
+            }
+            if (has_right)
+            {
+                is_pair x = ext;  // send_right: my last hl cells go to the right neighbour
+                x.lf[i] = x.ll[i] + 1 - hl;
+                x.gf[i] = x.gl[i] + 1 - hl;
+                send[i][a][right].push_back(x);
+                is_pair y = ext;  // recv_right
+                y.lf[i] = y.ll[i] + 1;
+                y.gf[i] = y.gl[i] + 1;
+                y.ll[i] += hr;
+                y.gl[i] += hr;
+                recv[i][a][right].push_back(y);
+            }
+            if (has_left)
+            {
+                is_pair x = ext;  // send_left: my first hr cells go to the left neighbour
+                x.ll[i] = x.lf[i] - 1 + hr;
+                x.gl[i] = x.gf[i] - 1 + hr;
+                send[i][a][left].push_back(x);
+            }
+            if (has_left)
+            {
+                ext.lf[i] -= hl;
+                ext.gf[i] -= hl;
+            }
+            if (has_right)
+            {
+                ext.ll[i] += hr;
+                ext.gl[i] += hr;
+            }
+        }
+    }
+    std::vector<std::vector<int>> by_rank(world);
+    for (int a = 0; a < n; ++a) by_rank[doms[a].rank].push_back(a);
+    out.assign(dim, pattern_set{});
+    for (int i = 0; i < dim; ++i)
+    {
+        // receivers' tags: (sender id, receiver id) -> tag
+        std::map<std::pair<int32_t, int32_t>, int32_t> tag_of;
+        int32_t my_max_tag = 0;
+        for (int r = 0; r < world; ++r)
+        {
+            std::map<int32_t, int32_t> last_tag;  // remote rank -> last tag handed out
+            for (int a : by_rank[r])
+                for (auto& kv : recv[i][a])
+                {
+                    const int32_t rr = doms[index_of[kv.first]].rank;
+                    auto it = last_tag.find(rr);
+                    const int32_t tag = it == last_tag.end() ? 0 : it->second + 1;
+                    last_tag[rr] = tag;
+                    tag_of[{kv.first, doms[a].id}] = tag;
+                    if (r == my_rank) my_max_tag = std::max(my_max_tag, tag);
+                }
+        }
+        auto& ps = out[i];
+        ps.kind = 0;
+        ps.dim = dim;
+        ps.max_tag = my_max_tag;
+        ps.my_rank = my_rank;
+        if (my_rank < 0 || my_rank >= world) continue;
+        for (int a : by_rank[my_rank])
+        {
+            domain_pattern p;
+            p.id = doms[a].id;
+            for (auto& kv : recv[i][a])
+            {
+                halo_entry e;
+                e.key = {kv.first, doms[index_of[kv.first]].rank, tag_of.at({kv.first, p.id})};
+                e.boxes = kv.second;
+                p.recv.push_back(std::move(e));
+            }
+            for (auto& kv : send[i][a])
+            {
+                auto t = tag_of.find({p.id, kv.first});
+                if (t == tag_of.end())
+                    throw std::runtime_error("staged pattern: inconsistent domain lookup (a "
+                                             "neighbour does not name this domain back)");
+                halo_entry e;
+                e.key = {kv.first, doms[index_of[kv.first]].rank, t->second};
+                e.boxes = kv.second;
+                p.send.push_back(std::move(e));
+            }
+            ps.doms.push_back(std::move(p));
+        }
+    }
+}
 }  // namespace ghx

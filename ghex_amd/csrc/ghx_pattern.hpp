@@ -58,6 +58,11 @@ int regular_make_pattern(int dim, const ghx_regular_domain* doms, int n, const i
                          const int32_t* glast, const int32_t* halos, const int32_t* periodic,
                          int my_rank, pattern_set& out);
 
+// make_staged_pattern (include/ghex/structured/regular/make_pattern.hpp:47-250): dim patterns
+void staged_make_pattern(int dim, const ghx_regular_domain* doms, int n, const int32_t* nbrs,
+                         const int32_t* gfirst, const int32_t* glast, const int32_t* halos,
+                         const int32_t* periodic, int my_rank, std::vector<pattern_set>& out);
+
 int unstructured_make_pattern(int n, const int32_t* ids, const int32_t* ranks,
                               const int64_t* gids, const int64_t* gid_counts,
                               const int64_t* outer_lids, const int64_t* outer_counts,

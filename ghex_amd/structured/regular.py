@@ -113,6 +113,62 @@ def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[Domain
     return PatternContainer(h.value, context, domain_range, "structured", D)
 
 
+def make_staged_pattern(context, domain_range: Sequence[DomainDescriptor], domain_lookup,
+                        global_first, global_last, halos, periodicity):
+    """make_staged_pattern(ctx, domains, d_lu, g_first, g_last, halos, periodic)
+    (include/ghex/structured/regular/make_pattern.hpp:47-250): one pattern container per
+    dimension; exchanging them in order (stage 0, then 1, ...) fills the whole halo including
+    edges and corners, stage i moving the dimension-i slabs over the box already extended by the
+    halos of the earlier stages.
+
+    domain_lookup(domain_id, offset) -> the neighbour at `offset` (a tuple with one -1/+1 entry):
+    an object with id() (and rank()), an (id, rank) pair, or an id. halos as for HaloGenerator
+    (per dimension an int or a (minus, plus) pair, or the flat list). Each rank evaluates the
+    look-up for its own domains; the tables are all-gathered once (the reference exchanges tag
+    lists over MPI instead, make_pattern.hpp:218-227)."""
+    hg = HaloGenerator(global_first, global_last, halos, periodicity)
+    D = hg.ndim
+
+    def nid(x):
+        if x is None:
+            return -1
+        if hasattr(x, "id"):
+            return int(x.id() if callable(x.id) else x.id)
+        if isinstance(x, (tuple, list)):
+            return int(x[0])
+        return int(x)
+
+    mine = []
+    for d in domain_range:
+        if d.ndim != D:
+            raise ValueError("domain and halo dimensions differ")
+        nb = []
+        for i in range(D):
+            for side in (-1, 1):
+                off = [0] * D
+                off[i] = side
+                h = hg.halos[2 * i + (0 if side < 0 else 1)]
+                nb.append(nid(domain_lookup(d.domain_id(), tuple(off))) if h > 0 else -1)
+        mine.append((d.domain_id(), d.first(), d.last(), nb))
+    gathered = context.all_gather_object(mine)
+    doms, nbrs = [], []
+    for r, lst in enumerate(gathered):
+        for (i, f, l, nb) in lst:
+            rd = _ghx.RegularDomain()
+            rd.id, rd.rank = i, r
+            for k in range(D):
+                rd.first[k], rd.last[k] = f[k], l[k]
+            doms.append(rd)
+            nbrs.extend(nb)
+    darr = (_ghx.RegularDomain * len(doms))(*doms)
+    hs = (ctypes.c_void_p * D)()
+    arr = _ghx.i32_array
+    _ghx.call("ghx_staged_pattern_create", D, darr, len(doms), arr(nbrs), arr(hg.global_first),
+              arr(hg.global_last), arr(hg.halos), arr([int(p) for p in hg.periodic]),
+              context.rank(), hs)
+    return [PatternContainer(hs[i], context, domain_range, "structured", D) for i in range(D)]
+
+
 def _layout_order(strides) -> tuple:
     """Layout map from strides (bindings/python/src/ghex/structured/regular.py:41-63): the
     largest stride gets 0, the smallest gets dim-1; ties broken to keep values unique."""

@@ -226,6 +226,18 @@ int ghx_regular_pattern_create(int32_t dim, const ghx_regular_domain* domains,
                                const int32_t* global_last, const int32_t* halos,
                                const int32_t* periodic, int32_t my_rank, ghx_pattern** out);
 
+/* make_staged_pattern (include/ghex/structured/regular/make_pattern.hpp:47-250): `dim` pattern
+ * handles written to out[0..dim-1], stage i exchanging the halos of dimension i over the domain
+ * box extended by the halos of stages 0..i-1 (exchanging the stages in order fills edges and
+ * corners). domains as for ghx_regular_pattern_create (all ranks); neighbors[(k*dim + i)*2 + s]
+ * = the id of domain k's left (s = 0) / right (s = 1) neighbour in dimension i — the reference's
+ * domain look-up `d_lu(id, offset)` evaluated for offset -1/+1 along i; only consulted where
+ * that side has a halo (non-zero width, and periodic or inside the global box). */
+int ghx_staged_pattern_create(int32_t dim, const ghx_regular_domain* domains, int32_t n_domains,
+                              const int32_t* neighbors, const int32_t* global_first,
+                              const int32_t* global_last, const int32_t* halos,
+                              const int32_t* periodic, int32_t my_rank, ghx_pattern** out);
+
 /* make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370) for rank
  * `my_rank`. For every domain d of every rank: gids[d] (storage order), the outer (halo) local
  * ids, and optionally the halo generator's gid list (NULL/-1 = all outer gids,

@@ -248,6 +248,78 @@ def regular_make_pattern(ranks_domains: Sequence[Sequence[RegularDomain]], gfirs
     return pats
 
 
+def staged_make_pattern(ranks_domains: Sequence[Sequence[RegularDomain]], lookup, gfirst, glast,
+                        halos, periodic) -> List[List[List[RegularPattern]]]:
+    """All-ranks restatement of structured::regular::make_staged_pattern
+    (include/ghex/structured/regular/make_pattern.hpp:47-250). lookup(id, offset) -> neighbour id.
+    Returns stages[i][r][k]: stage i exchanges the dimension-i slabs over the domain box extended
+    by the halos of stages < i (:90-181); tags per receiving rank and remote rank in pattern and
+    key order (:199-214); senders take the receiver's tag for (sender id, receiver id)
+    (:229-243); max_tag is the rank's own (:201, 227)."""
+    D = len(gfirst)
+    rank_of = {d.id: r for r, doms in enumerate(ranks_domains) for d in doms}
+    stages = [[[RegularPattern(d.id, r) for d in doms] for r, doms in enumerate(ranks_domains)]
+              for _ in range(D)]
+    raw = {}  # (stage, id) -> (recv {neighbour id: [ISPair]}, send {neighbour id: [ISPair]})
+    for doms in ranks_domains:
+        for d in doms:
+            lf = [0] * D
+            ll = [d.last[c] - d.first[c] for c in range(D)]
+            gf, gl = list(d.first), list(d.last)
+            for i in range(D):
+                hl, hr = halos[2 * i], halos[2 * i + 1]
+                has_left = hl > 0 and (periodic[i] or gf[i] - hl >= gfirst[i])
+                has_right = hr > 0 and (periodic[i] or gl[i] + hr <= glast[i])
+                recv, send = {}, {}
+
+                def box(a, b, c, e, dim=i):
+                    x = [list(lf), list(ll), list(gf), list(gl)]
+                    x[0][dim], x[1][dim], x[2][dim], x[3][dim] = a, b, c, e
+                    return ISPair(*(tuple(t) for t in x))
+                off_l = tuple(-1 if c == i else 0 for c in range(D))
+                off_r = tuple(1 if c == i else 0 for c in range(D))
+                if has_left:
+                    left = lookup(d.id, off_l)
+                    recv.setdefault(left, []).append(
+                        box(lf[i] - hl, lf[i] - 1, gf[i] - hl, gf[i] - 1))
+                if has_right:
+                    right = lookup(d.id, off_r)
+                    send.setdefault(right, []).append(
+                        box(ll[i] + 1 - hl, ll[i], gl[i] + 1 - hl, gl[i]))
+                    recv.setdefault(right, []).append(
+                        box(ll[i] + 1, ll[i] + hr, gl[i] + 1, gl[i] + hr))
+                if has_left:
+                    send.setdefault(left, []).append(
+                        box(lf[i], lf[i] - 1 + hr, gf[i], gf[i] - 1 + hr))
+                    lf[i] -= hl
+                    gf[i] -= hl
+                if has_right:
+                    ll[i] += hr
+                    gl[i] += hr
+                raw[(i, d.id)] = (recv, send)
+    for i in range(D):
+        tag_of = {}
+        for r, doms in enumerate(ranks_domains):
+            last, mt = {}, 0
+            for d in doms:
+                for nid in sorted(raw[(i, d.id)][0]):
+                    rr = rank_of[nid]
+                    last[rr] = last[rr] + 1 if rr in last else 0
+                    tag_of[(nid, d.id)] = last[rr]
+                    mt = max(mt, last[rr])
+            for p in stages[i][r]:
+                p.max_tag = mt
+        for r, doms in enumerate(ranks_domains):
+            for k, d in enumerate(doms):
+                recv, send = raw[(i, d.id)]
+                p = stages[i][r][k]
+                p.recv = {(nid, tag_of[(nid, d.id)]): (rank_of[nid], recv[nid])
+                          for nid in sorted(recv)}
+                p.send = {(nid, tag_of[(d.id, nid)]): (rank_of[nid], send[nid])
+                          for nid in sorted(send)}
+    return stages
+
+
 # --------------------------------------------------------------------------------------------
 # buffer planning: communication_object::allocate (communication_object.hpp:1003-1067)
 # --------------------------------------------------------------------------------------------
