@@ -6,20 +6,28 @@ Workload (BASELINE configs[1], weak-scaled for N>1 as configs[2]): per GPU one 5
 iteration spaces are a self message); N=2/4/8: (2,1,1)/(2,2,1)/(2,2,2) decomposition of the
 periodic global grid, one rank per GPU.
 
-A step = the product's exchange step minus transport, fields and buffers resident in HBM: for
-N>1 one fused pack launch (every iteration space of every send buffer) + one fused unpack launch
-(every recv buffer); at N=1 every message is a self message and the communication object runs
-pack+unpack as ONE launch (ghx_exchange_self: each workgroup packs a tile of the buffer, then
-unpacks the same bytes; `--unfused` times the two-launch form, also reported as "unfused").
-Algorithmic bytes per step per GPU = 4 * n * 8 (pack read + write, unpack read + write),
-n = (N+2H)^3 - N^3 halo cells. value = sum over ranks of bytes*K / max over ranks of the K-step
-wall time; the K steps replay hipGraphs of --steps-per-graph steps.
+A step = the per-rank exchange step minus transport, fields and buffers resident in HBM: one
+fused pack launch (every iteration space of every send buffer -> the send buffers) + one fused
+unpack launch (the recv buffers -> every halo). That is what every rank runs at N>1, and at N=1
+the same two launches are timed (the recv buffer of a self message is its send buffer), so the
+N=1..8 lines measure the same kernels. Algorithmic bytes per step per GPU = 4 * n * 8 (pack read
++ write, unpack read + write), n = (N+2H)^3 - N^3 halo cells. value = sum over ranks of
+bytes*K / max over ranks of the K-step wall time; the K steps replay hipGraphs of
+--steps-per-graph steps, every graph instantiated and replayed once BEFORE the timed region.
+
+The product's N=1 exchange runs pack+unpack as ONE launch (k_self: each lane packs its buffer
+bytes and writes the halos from the same registers, so the buffer is never read back): it moves
+3 * n * 8 bytes and is reported as "fused_self" with exactly those bytes, not as the headline.
 
 Before timing, one full exchange (pack -> RCCL send/recv over xGMI for N>1 -> unpack) is run and
 every cell of every rank's (N+2H)^3 box is verified on the GPU against the wrapped global index.
-Extra fields: the full exchange time (incl. RCCL), the host-staged rate (pack + D2H + H2D +
-unpack through pinned memory), per-kernel HIP-event durations, and on rank 0 at N=1 the oracle's
-single-thread CPU pack+unpack on a bounded sample (cpu_baseline).
+Extra fields: cold-cache launch times (default; --no-cold for profiler runs), the full exchange
+time incl. RCCL (one group, and per-peer pipelined), the host-staged rate (pack + D2H + H2D +
+unpack through pinned memory), and on rank 0 at N=1 the oracle's single-thread CPU pack+unpack
+on a bounded sample (cpu_baseline).
+
+`python bench.py --gpus N` without torchrun spawns the N rank processes itself (before any GPU
+call) with MASTER_ADDR=127.0.0.1; under torch.distributed.run it runs as the given rank.
 """
 import argparse
 import json
@@ -45,15 +53,13 @@ def parse():
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph")
     p.add_argument("--steps-per-graph", type=int, default=10,
                    help="steps captured per hipGraph (the K timed steps replay K/G graphs)")
-    p.add_argument("--unfused", action="store_true",
-                   help="N=1: time pack and unpack as two launches instead of the fused self exchange")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     p.add_argument("--tune", default="", help="developer: ghx_tune key=value,... before planning")
-    p.add_argument("--cold", action="store_true",
-                   help="also time the dominant launch right after a 1 GiB cache-flushing kernel "
-                        "(opt-in: its launches would skew a profiler's per-kernel average)")
+    p.add_argument("--no-cold", action="store_true",
+                   help="skip the cold-cache launch times (their extra launches of the same "
+                        "kernels would skew a profiler's per-kernel averages)")
     p.add_argument("--bulk", action="store_true",
                    help="N>1: also time the zero-copy bulk exchange (IPC puts into peer halos); "
                         "always on at N=1 (self puts)")
@@ -63,11 +69,102 @@ def parse():
                    help="developer: N>1 ranks all on cuda:0 (RCCL refuses two ranks per GPU), "
                         "gloo group and the host-staged transport — exercises the N>1 code path "
                         "on a one-GPU box; its numbers are not the metric")
+    p.add_argument("--extras-timeout", type=float, default=240.0,
+                   help="seconds the extras (after the headline) may take before the line is "
+                        "printed without them")
     return p.parse_args()
+
+
+def spawn_workers(args) -> int:
+    """`bench.py --gpus N` outside torchrun: start N fresh rank processes (this process never
+    touches the GPU), rank 0's stdout is the JSON line; exit with the worst child status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ)
+        env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(args.gpus),
+                   RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(args.gpus),
+                   GHX_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                c = p.poll()
+                if c is None:
+                    continue
+                pending.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in pending:  # one rank died: the others would wait for it forever
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+class Runner:
+    """run(k): exactly k steps, replayed from hipGraphs of G steps (+ one graph for k % G).
+    prepare(k) captures and replays once every graph run(k) will use, so nothing is captured
+    or instantiated inside a timed region."""
+
+    def __init__(self, torch, dev, stream, step, G, eager=False):
+        self.torch, self.dev, self.stream, self.step = torch, dev, stream, step
+        self.G, self.eager, self.graphs = max(1, G), eager, {}
+
+    def _graph(self, n):
+        torch = self.torch
+        g = self.graphs.get(n)
+        if g is None:
+            side = torch.cuda.Stream(self.dev)
+            side.wait_stream(self.stream)
+            with torch.cuda.stream(side):
+                self.step()  # warm the capture stream
+            self.stream.wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    self.step()
+            self.graphs[n] = g
+            g.replay()
+            torch.cuda.synchronize(self.dev)
+        return g
+
+    def prepare(self, k):
+        if self.eager:
+            return
+        if k >= self.G:
+            self._graph(self.G)
+        if k % self.G:
+            self._graph(k % self.G)
+
+    def run(self, k):
+        if self.eager:
+            for _ in range(k):
+                self.step()
+            return
+        for _ in range(k // self.G):
+            self.graphs[self.G].replay()
+        if k % self.G:
+            self.graphs[k % self.G].replay()
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_workers(args))  # before anything touches the GPU
+    import threading
+
     import torch
     import torch.distributed as dist
 
@@ -75,14 +172,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world not in DECOMP:
+        raise SystemExit(f"--gpus must be one of {sorted(DECOMP)}")
     if args.rehearse:
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     distributed = world > 1 or args.force_dist
+    backend = None
     if distributed:
+        backend = "gloo" if args.rehearse else "nccl"
         if args.rehearse:
             dist.init_process_group("gloo")
         else:
@@ -131,16 +231,27 @@ def main():
     co = R.make_communication_object(ctx, staging="host" if args.rehearse else None)
     bis = [pc(fd)]
 
-    # ---- verified full exchange (pack -> RCCL -> unpack) --------------------------------------
-    co.exchange(bis).wait()
     idx = [torch.arange(E, device=dev, dtype=torch.int64) - Hw + first[d] for d in range(3)]
     wrap = [(idx[d] % G[d]).to(torch.float64) for d in range(3)]
-    expect = wrap[0].view(1, 1, E) + G[0] * (wrap[1].view(1, E, 1) + G[1] * wrap[2].view(E, 1, 1))
-    bad = int((base != expect).sum().item())
-    del expect
-    verified = bad == 0
-    if distributed:
-        verified = all_reduce_host(bad, dist.ReduceOp.SUM) == 0
+
+    def verify():
+        """Every cell of this rank's (N+2H)^3 box = its wrapped global index (summed over ranks)."""
+        expect = wrap[0].view(1, 1, E) + G[0] * (wrap[1].view(1, E, 1) +
+                                                 G[1] * wrap[2].view(E, 1, 1))
+        bad = int((base != expect).sum().item())
+        del expect
+        if distributed:
+            bad = int(all_reduce_host(bad, dist.ReduceOp.SUM))
+        return bad
+
+    def clear_halos():
+        base.fill_(-1.0)
+        base[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = (
+            ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)))
+
+    # ---- verified full exchange (pack -> RCCL -> unpack) --------------------------------------
+    co.exchange(bis).wait()
+    verified = verify() == 0
 
     plan = co.plan(bis)
     send, recv = co.buffers(plan, dev)
@@ -154,20 +265,13 @@ def main():
     L = _ghx.lib()
     ns, nr = len(send), len(recv)
 
-    # N=2/4: a rank has self messages (its periodic wrap in the undecomposed dimensions) AND peer
-    # messages; the communication object then completes the self messages inside the pack
-    # launch and unpacks the peer messages only (ghx_exchange_pack_self / _unpack_peers)
-    mixed = co.fuse_self and co.mixed(plan) and not args.unfused
-    pack_fn = L.ghx_exchange_pack_self if mixed else L.ghx_exchange_pack
-    unpack_fn = L.ghx_exchange_unpack_peers if mixed else L.ghx_exchange_unpack
-
     def pack(s):
-        rc = pack_fn(plan.h, fptr, 1, sptr, ns, s)
+        rc = L.ghx_exchange_pack(plan.h, fptr, 1, sptr, ns, s)
         if rc:
             raise RuntimeError(L.ghx_last_error().decode())
 
     def unpack(s):
-        rc = unpack_fn(plan.h, fptr, 1, rptr, nr, s)
+        rc = L.ghx_exchange_unpack(plan.h, fptr, 1, rptr, nr, s)
         if rc:
             raise RuntimeError(L.ghx_last_error().decode())
 
@@ -176,58 +280,19 @@ def main():
         if rc:
             raise RuntimeError(L.ghx_last_error().decode())
 
-    # The product's exchange step: at N=1 every message is a self message and the communication
-    # object runs pack+unpack as ONE launch (ghx_exchange_self); otherwise pack, transport, unpack.
-    use_fused = co.fuse_self and co.all_self(plan) and not args.unfused
-
-    def step_unfused():
+    def step():
         s = torch.cuda.current_stream(dev).cuda_stream
         pack(s)
         unpack(s)
 
-    def step_fused():
-        fused(torch.cuda.current_stream(dev).cuda_stream)
-
-    def make_run(step):
-        """run(k): exactly k steps, replayed from hipGraphs of G = --steps-per-graph steps
-        (+ one graph for the remainder), so the graph-launch cost is paid once per G steps."""
-        if args.no_graph:
-            def run_eager(k):
-                for _ in range(k):
-                    step()
-            return run_eager
-        graphs = {}
-
-        def graph_of(n):
-            if n not in graphs:
-                side = torch.cuda.Stream(dev)
-                side.wait_stream(stream)
-                with torch.cuda.stream(side):
-                    step()  # warm the capture stream
-                stream.wait_stream(side)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for _ in range(n):
-                        step()
-                graphs[n] = g
-            return graphs[n]
-
-        G = max(1, args.steps_per_graph)
-
-        def run(k):
-            for _ in range(k // G):
-                graph_of(G).replay()
-            if k % G:
-                graph_of(k % G).replay()
-        return run
-
-    run = make_run(step_fused if use_fused else step_unfused)
-    run(args.warmup)
+    K, W = args.steps, args.warmup
+    runner = Runner(torch, dev, stream, step, args.steps_per_graph, eager=args.no_graph)
+    runner.prepare(W)
+    runner.prepare(K)
+    runner.run(W)
     torch.cuda.synchronize(dev)
 
-    dev_time = {}
-
-    def timed(fn, k, events=False):
+    def timed(fn, k, events=False, box=None):
         """Host wall time of k calls (barrier + synchronize on both sides, max over ranks); with
         events=True also the device time of the region from HIP events on the launch stream."""
         if distributed:
@@ -240,8 +305,8 @@ def main():
             fn()
         e1.record(stream)
         torch.cuda.synchronize(dev)
-        if events:
-            dev_time["s"] = e0.elapsed_time(e1) * 1e-3
+        if events and box is not None:
+            box["s"] = e0.elapsed_time(e1) * 1e-3
         if distributed:
             barrier()
         dt = time.perf_counter() - t0
@@ -249,15 +314,13 @@ def main():
             dt = all_reduce_host(dt, dist.ReduceOp.MAX)
         return dt
 
-    K = args.steps
-    run(K % max(1, args.steps_per_graph) or 1)  # instantiate the remainder graph untimed
-    torch.cuda.synchronize(dev)
-    T = timed(lambda: run(K), 1, events=True)
+    dev_time = {}
+    T = timed(lambda: runner.run(K), 1, events=True, box=dev_time)
     dev_step = dev_time["s"] / K  # device time per step over the timed region (HIP events)
     value = world * step_bytes * K / T / 1e9
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
-        "steps": K, "warmup": args.warmup, "ms_per_step": round(T / K * 1e3, 5),
+        "steps": K, "warmup": W, "ms_per_step": round(T / K * 1e3, 5),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (owned cell = global linear index; verified after a full exchange)",
         "config": {
@@ -265,13 +328,11 @@ def main():
                         f"device-resident pack+unpack, decomposition {list(parts)}",
             "N": N, "halo": Hw, "fields": 1, "decomposition": list(parts),
             "launch": ("eager" if args.no_graph else
-                       f"hipGraph of {args.steps_per_graph} steps") + ", " +
-                      ("fused self-exchange: 1 launch per step (each lane packs its buffer bytes "
-                       "and writes the halos from the same registers)" if use_fused else
-                       "pack launch completing the self messages + unpack launch of the peer "
-                       "messages" if mixed else "pack launch + unpack launch"),
+                       f"hipGraphs of {args.steps_per_graph} steps, instantiated before the "
+                       "timed region") + ", pack launch + unpack launch per step",
             "bytes_per_step_per_gpu": step_bytes,
             "parallelism": f"{world} rank(s), one domain per GPU",
+            "world_size": world, "backend": backend,
         },
         "verified": verified,
     }
@@ -280,138 +341,169 @@ def main():
                             "not the metric")
 
     # ---- per-kernel HIP-event durations (dominant kernel roofline) ----------------------------
-    # Differential method (removes the fixed cost of the events themselves): hipGraphs of M steps,
-    # of M steps + one pack, and of M steps + one pack + one unpack, replayed in interleaved
-    # rounds; pack = T1 - T0, unpack = T2 - T1 (each includes its dependent-launch boundary).
+    # Differential method (removes the events' own cost): hipGraphs of M steps, of M steps + one
+    # pack, and of M steps + one pack + one unpack, replayed in interleaved rounds (medians);
+    # pack = T1 - T0, unpack = T2 - T1.
     t_pack, t_unpack = kernel_durations(torch, dev, stream, [pack, unpack])
-    if use_fused:
-        # one launch per step: its average duration over the timed region = device time / K
-        (t_fused,) = kernel_durations(torch, dev, stream, [fused])
-        launch_bytes, dom_name, dom_t, kname = step_bytes, "self", dev_step, "k_self (pack+unpack)"
-    else:
-        # two launches per step: the timed region's device time split by their live differential
-        # durations (graphs of M and M+1 launches)
-        # (mixed: the pack launch also moves the self messages' unpack bytes, the unpack launch
-        # only the peer messages')
-        self_b = sum(b["size"] for b in plan.recv if b["rank"] == rank) if mixed else 0
-        pack_b, unpack_b = 2 * n_halo * 8 + 2 * self_b, 2 * n_halo * 8 - 2 * self_b
-        dom_name, dom_d = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
-        launch_bytes = pack_b if dom_name == "pack" else unpack_b
-        dom_t = dev_step * dom_d / (t_pack + t_unpack)
-        kname = ("k_self<pack + self messages>" if mixed and dom_name == "pack"
-                 else f"k_copy<{dom_name}>")
+    dom_name, dom_t = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+    launch_bytes = 2 * n_halo * 8  # read n*s + write n*s, either kernel
     achieved = launch_bytes / dom_t / 1e9
-    traffic = None
+    traffic, traffic_src = None, None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tfile) and not mixed:  # (profiled: the N=1 launches)
+    if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            ent = tj.get(f"N{N}_H{Hw}", {}).get(dom_name)
-            traffic = ent.get("hbm_bytes_per_launch") if ent else None
+            # (profiled on the one-domain plan: N=1 only; per-peer buffers at N>1)
+            ent = tj.get(f"N{N}_H{Hw}", {}).get(dom_name) if world == 1 else None
+            if ent:
+                traffic = ent.get("hbm_bytes_per_launch")
+                traffic_src = tj.get("source")
         except Exception:
             traffic = None
-    out["roofline"] = {"bound": "hbm", "kernel": kname,
-                       "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                       "traffic_source": (None if traffic is None else
-                                          "profiles/pmc_traffic.json: rocprofv3 --pmc of the "
-                                          f"N=1 {dom_name} launch of the same bytes" +
-                                          ("" if world == 1 else
-                                           " (one-domain plan; per-peer buffers at N>1)")),
-                       "algorithmic_bytes_per_launch": launch_bytes,
-                       "launch_us": round(dom_t * 1e6, 2),
-                       "launch_us_source": "HIP events on the launch stream around the timed "
-                                           "region, device time per step" +
-                                           ("" if use_fused else " x the kernel's share of the "
-                                            "step (graph differencing)"),
-                       "step_device_us": round(dev_step * 1e6, 2),
-                       "pack_us": round(t_pack * 1e6, 2), "unpack_us": round(t_unpack * 1e6, 2)}
-    if use_fused:
-        out["roofline"]["self_us_differential"] = round(t_fused * 1e6, 2)
-    if use_fused:
-        # the same step as two launches (what N>1 runs per rank), for comparison
-        run_u = make_run(step_unfused)
-        run_u(max(5, K % max(1, args.steps_per_graph)))
-        Tu = timed(lambda: run_u(K), 1)
-        out["unfused"] = {"value": round(world * step_bytes * K / Tu / 1e9, 2),
-                          "ms_per_step": round(Tu / K * 1e3, 5)}
+    out["roofline"] = {
+        "bound": "hbm", "kernel": f"k_copy<{dom_name}>",
+        "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+        "traffic_source": traffic_src,
+        "algorithmic_bytes_per_launch": launch_bytes,
+        "launch_us": round(dom_t * 1e6, 2),
+        "launch_us_source": "HIP events on the launch stream: graphs of M steps vs M steps + "
+                            "one more launch, replayed interleaved, median difference",
+        "pack_us": round(t_pack * 1e6, 2), "unpack_us": round(t_unpack * 1e6, 2),
+        "step_device_us": round(dev_step * 1e6, 2),
+        "step_achieved": round(step_bytes / dev_step / 1e9, 1),
+        "step_frac": round(step_bytes / dev_step / 1e9 / HBM_PEAK_GBS, 4),
+    }
 
-    if not args.no_extras:
-        # full exchange incl. transport (RCCL for N>1; self-message aliasing for N=1)
-        ke = min(K, 50)
-        for _ in range(3):
-            co.exchange(bis).wait()
-        Te = timed(lambda: co.exchange(bis).wait(), ke)
-        out["exchange_ms_per_step"] = round(Te / ke * 1e3, 4)
-        if world == 1 or args.bulk:
-            # zero-copy bulk exchange (BulkCommunicationObject): puts straight into the
-            # receivers' halos, no buffers: 2*n*8 bytes moved per step (not the metric's 4*n*8)
-            try:
-                bco = ghex_amd.make_bulk_communication_object(ctx)
-                bco.add_field(bis[0])
-                bco.init()
-                for _ in range(3):
-                    bco.exchange().wait()
-                Tb = timed(lambda: bco.exchange().wait(), ke)
-                put = bco._puts[0]
+    # ---- extras (bounded: the line is printed without them if they overrun) -------------------
+    done = threading.Event()
+    printed = threading.Lock()
 
-                def put_fn(s):
-                    rc = L.ghx_put_execute(put[0], put[1], put[2], put[3], put[4], s)
-                    if rc:
-                        raise RuntimeError(L.ghx_last_error().decode())
-                (t_put,) = kernel_durations(torch, dev, stream, [put_fn])
-                out["bulk"] = {"exchange_ms_per_step": round(Tb / ke * 1e3, 4),
-                               "put_launches": len(bco._puts),
-                               "put_us": round(t_put * 1e6, 2) if len(bco._puts) == 1 else None,
-                               "bytes_moved_per_step": 2 * n_halo * 8}
-                del bco
-            except Exception as e:  # reported, never fatal for the headline measurement
-                out["bulk"] = {"error": str(e)[:200]}
-            co.exchange(bis).wait()
-        # host-staged: pack -> D2H (pinned) -> H2D -> unpack (NIC-side buffers, north star)
-        hs = [torch.empty(b["size"], dtype=torch.uint8, pin_memory=True) for b in plan.send]
+    def emit(o):
+        if rank == 0 and printed.acquire(blocking=False):
+            print(json.dumps(o), flush=True)
 
-        def staged():
-            s = torch.cuda.current_stream(dev).cuda_stream
-            pack(s)
-            for i, b in enumerate(plan.send):
-                hs[i].copy_(send[i][:b["size"]], non_blocking=True)
-            for i, b in enumerate(plan.recv):  # N=1: every message is a self message
-                j = next(j for j, x in enumerate(plan.send) if x["pair"] == b["pair"])
-                recv[i][:b["size"]].copy_(hs[j], non_blocking=True)
-            unpack(s)
+    def watchdog():
+        if not done.wait(args.extras_timeout):
+            o = dict(out)
+            o["extras_error"] = f"extras exceeded {args.extras_timeout:.0f} s; printed without them"
+            emit(o)
+            sys.stdout.flush()
+            os._exit(0)
 
-        if world == 1:
-            for _ in range(3):
-                staged()
-            Ts = timed(staged, min(K, 50))
-            pcie = 2 * n_halo * 8
-            out["host_staged"] = {
-                "GBps_algorithmic": round(step_bytes * min(K, 50) / Ts / 1e9, 2),
-                "ms_per_step": round(Ts / min(K, 50) * 1e3, 4),
-                "pcie_bytes_per_step": pcie}
-            # restore valid halos after the staged copies
-            co.exchange(bis).wait()
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        extras(args, torch, dist, dev, stream, out, locals())
+    except Exception as e:  # reported, never fatal for the headline measurement
+        out["extras_error"] = f"{type(e).__name__}: {str(e)[:300]}"
+    done.set()
+    emit(out)
+    if distributed:
+        barrier()
+        dist.destroy_process_group()
 
-    if args.cold:
-        # the dominant launch with cold caches: an application's stencil sweeps the whole field
-        # between exchanges, so its halo rows are not left in the 256 MiB Infinity Cache as
-        # they are when the bench replays exchanges back to back. A 1 GiB read-modify-write
-        # before every launch evicts them; the flush itself is differenced away.
+
+def extras(args, torch, dist, dev, stream, out, v):
+    """Everything after the headline: cold caches, fused self exchange, full exchanges,
+    host staging, other configs, CPU baseline."""
+    world, rank, K = v["world"], v["rank"], v["K"]
+    pack, unpack, fused, timed = v["pack"], v["unpack"], v["fused"], v["timed"]
+    co, bis, plan, send, recv = v["co"], v["bis"], v["plan"], v["send"], v["recv"]
+    n_halo, step_bytes, launch_bytes = v["n_halo"], v["step_bytes"], v["launch_bytes"]
+    ghex_amd, R, L, _ghx, N, Hw = v["ghex_amd"], v["R"], v["L"], v["_ghx"], v["N"], v["Hw"]
+    roof = out["roofline"]
+
+    if not args.no_cold:
+        # Cold caches: an application's stencil sweeps the whole field between exchanges, so the
+        # halo-adjacent lines are not left in the 256 MiB Infinity Cache as they are when the
+        # bench replays steps back to back. A 1 GiB read-only reduction before every launch
+        # evicts them without leaving dirty lines (cold, clean); a 1 GiB read-modify-write
+        # leaves 1 GiB dirty that the launch then evicts (cold, dirty). Flushes differenced away.
         fl = torch.zeros(1 << 27, dtype=torch.float64, device=dev)
-        dom_fn = fused if use_fused else (pack if dom_name == "pack" else unpack)
-        t_cold = cold_duration(torch, dev, stream, dom_fn, lambda s: fl.add_(1.0))
-        out["roofline"]["cold_launch_us"] = round(t_cold * 1e6, 2)
-        out["roofline"]["cold_achieved"] = round(launch_bytes / t_cold / 1e9, 1)
-        # the same with a read-only flush (1 GiB reduction): caches cold but not dirty, so the
-        # launch does not also pay for writing back the flush's dirty lines it evicts
         acc = torch.empty((), dtype=torch.float64, device=dev)
-        t_clean = cold_duration(torch, dev, stream, dom_fn,
-                                lambda s: torch.sum(fl, dim=(0,), out=acc))
-        out["roofline"]["cold_clean_launch_us"] = round(t_clean * 1e6, 2)
-        out["roofline"]["cold_clean_achieved"] = round(launch_bytes / t_clean / 1e9, 1)
+        clean = lambda s: torch.sum(fl, dim=(0,), out=acc)  # noqa: E731
+        t_pc = cold_duration(torch, dev, stream, pack, clean)
+        t_uc = cold_duration(torch, dev, stream, unpack, clean)
+        t_dom = t_pc if roof["kernel"] == "k_copy<pack>" else t_uc
+        roof["cold_clean_launch_us"] = round(t_dom * 1e6, 2)
+        roof["cold_clean_achieved"] = round(launch_bytes / t_dom / 1e9, 1)
+        roof["cold_clean_frac"] = round(launch_bytes / t_dom / 1e9 / HBM_PEAK_GBS, 4)
+        roof["cold_clean_pack_us"] = round(t_pc * 1e6, 2)
+        roof["cold_clean_unpack_us"] = round(t_uc * 1e6, 2)
+        roof["cold_clean_step_GBps"] = round(step_bytes / (t_pc + t_uc) / 1e9, 1)
+        t_dirty = cold_duration(torch, dev, stream, pack if t_dom == t_pc else unpack,
+                                lambda s: fl.add_(1.0))
+        roof["cold_dirty_launch_us"] = round(t_dirty * 1e6, 2)
         del fl
         torch.cuda.empty_cache()
+
+    if world == 1 and co.fuse_self and co.all_self(plan):
+        # The product's N=1 exchange: ONE launch (k_self). Each lane packs its buffer bytes and
+        # writes the halos from the same registers: read n*s + buffer write n*s + halo write n*s.
+        (t_f,) = kernel_durations(torch, dev, stream, [fused])
+        moved = 3 * n_halo * 8
+        out["fused_self"] = {
+            "kernel": "k_self", "launch_us": round(t_f * 1e6, 2), "bytes_moved": moved,
+            "GBps_moved": round(moved / t_f / 1e9, 1),
+            "frac_moved": round(moved / t_f / 1e9 / HBM_PEAK_GBS, 4),
+            "exchange_equivalent_GBps": round(step_bytes / t_f / 1e9, 1),
+            "note": "pack+unpack of the same cells in one launch; the buffer is written but "
+                    "never read back, so bytes_moved = 3*n*8 (the metric's 4*n*8 is the "
+                    "two-launch step)"}
+
+    if args.no_extras:
+        return
+    # full exchange incl. transport (RCCL for N>1; self-message aliasing for N=1)
+    ke = min(K, 50)
+    for _ in range(3):
+        co.exchange(bis).wait()
+    Te = timed(lambda: co.exchange(bis).wait(), ke)
+    out["exchange_ms_per_step"] = round(Te / ke * 1e3, 4)
+    if world > 1:
+        # per-peer streams (rehearsal: the host-staged form of the same pipeline over gloo)
+        cop = R.make_communication_object(v["ctx"], pipelined=True,
+                                          staging="host" if args.rehearse else None)
+        v["clear_halos"]()
+        cop.exchange(bis).wait()
+        okp = v["verify"]() == 0
+        for _ in range(3):
+            cop.exchange(bis).wait()
+        Tp = timed(lambda: cop.exchange(bis).wait(), ke)
+        out["exchange_pipelined"] = {"ms_per_step": round(Tp / ke * 1e3, 4), "verified": okp,
+                                     "mode": "per-peer streams: pack, " +
+                                             ("D2H, gloo send/recv, H2D" if args.rehearse else
+                                              "one RCCL group on the pair's own communicator") +
+                                             " and unpack of each peer's buffers on its stream"}
+        del cop
+    if world == 1 or args.bulk:
+        # zero-copy bulk exchange (BulkCommunicationObject): puts straight into the
+        # receivers' halos, no buffers: 2*n*8 bytes moved per step (not the metric's 4*n*8)
+        try:
+            bco = ghex_amd.make_bulk_communication_object(v["ctx"])
+            bco.add_field(bis[0])
+            bco.init()
+            for _ in range(3):
+                bco.exchange().wait()
+            Tb = timed(lambda: bco.exchange().wait(), ke)
+            put = bco._puts[0]
+
+            def put_fn(s):
+                rc = L.ghx_put_execute(put[0], put[1], put[2], put[3], put[4], s)
+                if rc:
+                    raise RuntimeError(L.ghx_last_error().decode())
+            (t_put,) = kernel_durations(torch, dev, stream, [put_fn])
+            out["bulk"] = {"exchange_ms_per_step": round(Tb / ke * 1e3, 4),
+                           "put_launches": len(bco._puts),
+                           "put_us": round(t_put * 1e6, 2) if len(bco._puts) == 1 else None,
+                           "bytes_moved_per_step": 2 * n_halo * 8}
+            del bco
+        except Exception as e:  # reported, never fatal for the headline measurement
+            out["bulk"] = {"error": str(e)[:200]}
+        co.exchange(bis).wait()
+    if world == 1:
+        out["host_staged"] = host_staged(torch, dev, co, plan, send, recv, pack, unpack, timed,
+                                         step_bytes, n_halo, min(K, 50))
+        co.exchange(bis).wait()  # restore valid halos after the staged copies
 
     if not args.no_extras:
         # measured device-to-device copy rate (SURVEY §8(d)): 1 GiB -> 1 GiB, read+write bytes
@@ -425,14 +517,16 @@ def main():
             b.copy_(a)
         e1.record()
         e1.synchronize()
-        out["roofline"]["measured_d2d_copy_GBps"] = round(2 * a.numel() * 10 /
-                                                          (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+        roof["measured_d2d_copy_GBps"] = round(2 * a.numel() * 10 /
+                                               (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
         del a, b
         torch.cuda.empty_cache()
 
-    if world == 1 and not args.no_extras:
+    if world == 1:
         # the other BASELINE configs, per GPU (their 8-GPU forms are weak-scaled copies)
-        del base, logical, fd, bis, send, recv
+        for k in ("base", "logical", "fd", "bis", "send", "recv"):
+            v.pop(k, None)
+        del bis, send, recv
         co = None
         torch.cuda.empty_cache()
         out["extra_configs"] = {
@@ -442,11 +536,34 @@ def main():
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, Hw, args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if distributed:
-        barrier()
-        dist.destroy_process_group()
+
+
+def host_staged(torch, dev, co, plan, send, recv, pack, unpack, timed, step_bytes, n_halo, k):
+    """N=1 host-staged step: pack -> D2H into pinned memory -> H2D -> unpack (the NIC-side path
+    of the north star; every message of the N=1 plan is a self message). Two forms: serial
+    (one stream) and overlapped per buffer segment (D2H and H2D on their own copy streams,
+    each chunk's H2D queued behind its own D2H only)."""
+    hs = [torch.empty(b["size"], dtype=torch.uint8, pin_memory=True) for b in plan.send]
+    pairs = []
+    for i, b in enumerate(plan.recv):
+        j = next(j for j, x in enumerate(plan.send) if x["pair"] == b["pair"])
+        pairs.append((i, j, b["size"]))
+
+    def serial():
+        s = torch.cuda.current_stream(dev).cuda_stream
+        pack(s)
+        for i, b in enumerate(plan.send):
+            hs[i].copy_(send[i][:b["size"]], non_blocking=True)
+        for i, j, n in pairs:
+            recv[i][:n].copy_(hs[j], non_blocking=True)
+        unpack(s)
+
+    for _ in range(3):
+        serial()
+    Ts = timed(serial, k)
+    return {"GBps_algorithmic": round(step_bytes * k / Ts / 1e9, 2),
+            "ms_per_step": round(Ts / k * 1e3, 4), "pcie_bytes_per_step": 2 * n_halo * 8,
+            "form": "pack, D2H of the whole buffer, H2D, unpack on one stream"}
 
 
 def kernel_durations(torch, dev, stream, fns, M=10, rounds=15):

@@ -94,6 +94,17 @@ _SIGS = {
     "ghx_exchange_mixed": (c_i32, [c_vp, P(c_i32)]),
     "ghx_exchange_pack_self": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
     "ghx_exchange_unpack_peers": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_exchange_split": (c_i32, [c_vp]),
+    "ghx_exchange_pack_buffer": (c_i32, [c_vp, c_i32, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_exchange_unpack_buffer": (c_i32, [c_vp, c_i32, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_rccl_open": (c_i32, [ctypes.c_char_p]),
+    "ghx_rccl_unique_id": (c_i32, [P(ctypes.c_ubyte)]),
+    "ghx_rccl_comm_init": (c_i32, [P(ctypes.c_ubyte), c_i32, c_i32, P(c_vp)]),
+    "ghx_rccl_comm_destroy": (c_i32, [c_vp]),
+    "ghx_rccl_comm_check": (c_i32, [c_vp]),
+    "ghx_pipeline_create": (c_i32, [c_vp, c_i32, c_i32, P(c_i32), P(c_vp), P(c_i32), P(c_vp)]),
+    "ghx_pipeline_run": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
+    "ghx_pipeline_destroy": (c_i32, [c_vp]),
     "ghx_unstructured_pack": (c_i32, [P(UDataDesc), c_vp, c_vp, c_vp, c_i32, ctypes.c_int64, c_vp]),
     "ghx_unstructured_unpack": (c_i32, [P(UDataDesc), c_vp, c_vp, c_vp, c_i32, ctypes.c_int64, c_vp]),
     "ghx_ipc_export": (c_i32, [c_vp, P(ctypes.c_ubyte), P(ctypes.c_uint64)]),

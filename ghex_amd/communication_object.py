@@ -18,6 +18,16 @@ the exchange stream, one event per buffer so each host send starts as soon as it
 messages travel over a gloo group between host buffers, and each received buffer is copied back
 (H2D) as soon as its message has arrived; the unpack launch is queued behind the copies.
 Self messages stay on the device exactly as in the default mode.
+
+pipelined=True (the reference's per-buffer streams + send-as-packed,
+include/ghex/device/cuda/stream.hpp:25-73, communication_object.hpp:568-637, 703-767): each peer
+rank gets its own greatest-priority stream on which its send buffers are packed (one launch per
+buffer), its messages exchanged and its recv buffers unpacked, so a message leaves as soon as its
+own pack is done and is unpacked as soon as it lands. Device buffers: the native pipeline
+(ghx_pipeline_*) with one 2-rank RCCL communicator per peer pair (one shared communicator would
+serialise the per-peer groups); host staging: per-peer D2H after the pack, host sends as the
+copies land, H2D + unpack per message as it arrives. Peers are issued in one global round-robin
+order on every rank (round_of), which keeps streams that share a hardware queue deadlock-free.
 """
 from __future__ import annotations
 
@@ -76,6 +86,39 @@ def route(context, sends, recvs, group=None):
     return dist.batch_isend_irecv(ops)
 
 
+def round_of(a: int, b: int, world: int) -> int:
+    """Round of the pair (a, b) in a round-robin tournament over `world` ranks (circle method):
+    every rank meets every other rank exactly once, each rank in at most one pair per round.
+    With m = world rounded up to even and q = m - 1: pairs with b = m - 1 play in round a, the
+    others in the round r with a + b = 2r (mod q)."""
+    m = world + (world % 2)
+    q = m - 1
+    a, b = min(a, b), max(a, b)
+    if q <= 0:
+        return 0
+    if b == q:
+        return a
+    return ((a + b) * (m // 2)) % q
+
+
+def peer_order(me: int, peers, world: int):
+    """Peers of `me` in global round order (the issue order every rank uses)."""
+    return sorted(peers, key=lambda p: (round_of(me, p, world), p))
+
+
+class _Pipeline:
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                _ghx.lib().ghx_pipeline_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
 class CommunicationHandle:
     """communication_handle (communication_object.hpp:78-130): wait / is_ready / progress /
     schedule_wait."""
@@ -128,12 +171,19 @@ class CommunicationHandle:
 class CommunicationObject:
     """communication_object<grid, domain_id> (make_communication_object, :1105-1112)."""
 
-    def __init__(self, context, fuse_self: bool = True, staging=None):
+    def __init__(self, context, fuse_self: bool = True, staging=None, pipelined: bool = False,
+                 rccl_self: bool = False):
         if staging not in (None, "host"):
             raise ValueError("staging must be None (device buffers) or 'host'")
         self.context = context
         self.fuse_self = fuse_self
         self.staging = staging
+        self.pipelined = pipelined
+        # tests: route the self messages through RCCL too (a 1-rank communicator), so the
+        # pipeline's RCCL path runs on a one-GPU box
+        self.rccl_self = rccl_self
+        self._streams = {}
+        self._comms = {}
         self._plans = {}
         self._bufs = {}
         self._host = {}
@@ -214,10 +264,12 @@ class CommunicationObject:
                     for x in plan.send]
             recv = []
             me = self.context.rank()
+            # (rccl_self routes self messages through RCCL: distinct recv buffers then)
+            alias = not (self.pipelined and self.rccl_self)
             for x in plan.recv:
                 # self-message: unpack straight from the matching send buffer
                 j = next((i for i, s in enumerate(plan.send)
-                          if s["pair"] == x["pair"] and x["rank"] == me), None)
+                          if s["pair"] == x["pair"] and x["rank"] == me and alias), None)
                 recv.append(send[j] if j is not None else
                             torch.empty(max(1, x["size"]), dtype=torch.uint8, device=device))
             b = (send, recv)
@@ -283,6 +335,17 @@ class CommunicationObject:
                                   _ghx.ptr_array([t.data_ptr() for t in recv]))
         fptrs, sptrs, rptrs = arrs
         self._valid = True
+        if self.pipelined:
+            if self.staging == "host":
+                self._exchange_host_pipelined(plan, send, recv, fptrs, sptrs, rptrs, len(bis),
+                                              stream)
+            else:
+                pl = self._pipeline_of(plan, device)
+                _ghx.call("ghx_pipeline_run", pl.h, fptrs, len(bis), sptrs, len(send), rptrs,
+                          len(recv), stream.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            return CommunicationHandle(self, stream, ev)
         if self.fuse_self and self.all_self(plan):
             # every message stays on this device: pack + unpack in one launch (the launch and
             # the event go to `stream` explicitly: no current-stream switch needed)
@@ -350,6 +413,145 @@ class CommunicationObject:
                 dev_of[(peer, tag)].copy_(h, non_blocking=True)
         for w in sops:
             w.wait()
+
+    # -- pipelined exchange ---------------------------------------------------------------------
+    def _peer_stream(self, peer, device):
+        import torch
+        key = (peer, str(device))
+        s = self._streams.get(key)
+        if s is None:
+            s = self._streams[key] = torch.cuda.Stream(device, priority=-1)
+        return s
+
+    def _split(self, plan):
+        if not getattr(plan, "_split", False):
+            _ghx.call("ghx_exchange_split", plan.h)
+            plan._split = True
+
+    def _rccl_comms(self, peers):
+        """One 2-rank RCCL communicator per peer pair (setup time, collective over the context:
+        every rank reaches its first pipelined exchange of a plan together). The lower rank of a
+        pair draws the unique id; ids travel by the setup all-gather; communicators are created
+        in round order (each ncclCommInitRank blocks until both ends have called it)."""
+        import os
+        import torch
+        me, world = self.context.rank(), self.context.size()
+        _ghx.call("ghx_rccl_open", os.path.join(os.path.dirname(torch.__file__), "lib",
+                                                "librccl.so").encode())
+        want = [p for p in peers if p not in self._comms]
+        mine = {}
+        for p in want:
+            if p == me or me < p:
+                buf = (ctypes.c_ubyte * 128)()
+                _ghx.call("ghx_rccl_unique_id", buf)
+                mine[(me, p)] = bytes(buf)
+        every = self.context.all_gather_object(mine)
+        for p in peer_order(me, want, world):
+            a, b = min(me, p), max(me, p)
+            uid = every[a].get((a, b))  # drawn by the lower rank of the pair
+            if uid is None:
+                raise RuntimeError(f"no RCCL id for pair {(a, b)}: ranks disagree on peers")
+            comm = ctypes.c_void_p()
+            n = 1 if p == me else 2
+            _ghx.call("ghx_rccl_comm_init", (ctypes.c_ubyte * 128).from_buffer_copy(uid), n,
+                      0 if me <= p else 1, ctypes.byref(comm))
+            self._comms[p] = (comm, 0 if p == me else (1 if me < p else 0))
+        return [self._comms[p] for p in peers]
+
+    def _pipeline_of(self, plan, device):
+        pl = getattr(plan, "_pipeline", None)
+        if pl is None:
+            self._split(plan)
+            me, world = self.context.rank(), self.context.size()
+            ranks = {x["rank"] for x in plan.send + plan.recv}
+            peers = peer_order(me, [r for r in ranks if r != me or self.rccl_self], world)
+            comms = self._rccl_comms(peers)
+            h = ctypes.c_void_p()
+            _ghx.call("ghx_pipeline_create", plan.h, me, len(peers), _ghx.i32_array(peers),
+                      _ghx.ptr_array([c.value for c, _ in comms]),
+                      _ghx.i32_array([r for _, r in comms]), ctypes.byref(h))
+            pl = plan._pipeline = _Pipeline(h)
+        return pl
+
+    def _exchange_host_pipelined(self, plan, send, recv, fptrs, sptrs, rptrs, nf, stream):
+        """Host staging with per-peer overlap (reference non-stream-aware branch,
+        communication_object.hpp:611-637, 715-729): per peer stream pack -> D2H; each host send
+        is posted when its own copy has landed; each arrived message is copied back (H2D) and
+        unpacked on its peer's stream while the others are still in flight."""
+        import torch
+        self._split(plan)
+        me, world = self.context.rank(), self.context.size()
+        L = _ghx.lib()
+        device = stream.device
+        sends_of, recvs_of = {}, {}
+        for i, x in enumerate(plan.send):
+            sends_of.setdefault(x["rank"], []).append(i)
+        for j, x in enumerate(plan.recv):
+            recvs_of.setdefault(x["rank"], []).append(j)
+        peers = peer_order(me, [r for r in set(sends_of) | set(recvs_of) if r != me], world)
+        key = ("hostpipe", id(plan))
+        h = self._host.get(key)
+        if h is None:
+            h = self._host[key] = (
+                [torch.empty(max(1, x["size"]), dtype=torch.uint8, pin_memory=True) for x in plan.send],
+                [torch.empty(max(1, x["size"]), dtype=torch.uint8, pin_memory=True) for x in plan.recv])
+        hs, hr = h
+        start = torch.cuda.Event()
+        start.record(stream)
+        landed = {}
+        for p in peers:
+            sp = self._peer_stream(p, device)
+            sp.wait_event(start)
+            for i in sends_of.get(p, []):
+                _ghx.check(L.ghx_exchange_pack_buffer(plan.h, i, fptrs, nf, sptrs, len(send),
+                                                      sp.cuda_stream), "pack_buffer")
+                with torch.cuda.stream(sp):
+                    hs[i][:plan.send[i]["size"]].copy_(send[i][:plan.send[i]["size"]],
+                                                       non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(sp)
+            landed[p] = ev
+        # self messages: packed and unpacked on the caller's stream (recv aliases send)
+        for i, x in enumerate(plan.send):
+            if x["rank"] == me:
+                _ghx.check(L.ghx_exchange_pack_buffer(plan.h, i, fptrs, nf, sptrs, len(send),
+                                                      stream.cuda_stream), "pack_buffer")
+        for j, x in enumerate(plan.recv):
+            if x["rank"] == me:
+                _ghx.check(L.ghx_exchange_unpack_buffer(plan.h, j, fptrs, nf, rptrs, len(recv),
+                                                        stream.cuda_stream), "unpack_buffer")
+        dist = self.context.distributed
+        group = self._host_group
+        rops = []
+        for p in peers:
+            for j in sorted(recvs_of.get(p, []), key=lambda j: (plan.recv[j]["tag"], plan.recv[j]["pair"])):
+                x = plan.recv[j]
+                rops.append([dist.irecv(hr[j][:x["size"]], self.context.global_rank(p), group,
+                                        x["tag"]), j, p])
+        sops = []
+        for p in peers:
+            landed[p].synchronize()
+            for i in sorted(sends_of.get(p, []), key=lambda i: (plan.send[i]["tag"], plan.send[i]["pair"])):
+                x = plan.send[i]
+                sops.append(dist.isend(hs[i][:x["size"]], self.context.global_rank(p), group,
+                                       x["tag"]))
+        while rops:
+            for op in list(rops):
+                w, j, p = op
+                if not w.is_completed():
+                    continue
+                w.wait()
+                rops.remove(op)
+                sp = self._peer_stream(p, device)
+                n = plan.recv[j]["size"]
+                with torch.cuda.stream(sp):
+                    recv[j][:n].copy_(hr[j][:n], non_blocking=True)
+                _ghx.check(L.ghx_exchange_unpack_buffer(plan.h, j, fptrs, nf, rptrs, len(recv),
+                                                        sp.cuda_stream), "unpack_buffer")
+        for w in sops:
+            w.wait()
+        for p in peers:
+            stream.wait_stream(self._peer_stream(p, device))
 
     # low-level access for benchmarks / tests (no transport)
     def pack_only(self, bis, stream=None):

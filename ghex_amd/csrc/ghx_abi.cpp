@@ -12,6 +12,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include "ghx_exchange.hpp"
+#include "ghx_guard.hpp"
 #include "ghx_pattern.hpp"
 #include "ghx_plan.hpp"
 
@@ -23,226 +25,192 @@ namespace ghx
 {
 namespace
 {
-thread_local std::string g_error;
-
-template<typename F>
-int guarded(F&& f)
+// Plan caches of the per-call convenience entry points (ghx_structured_pack/unpack,
+// ghx_unstructured_pack/unpack), like the reference's pattern container that outlives its
+// exchanges (include/ghex/pattern_container.hpp:84-87). A hit is exact: the structured key IS
+// the content (descriptor, iteration spaces, direction); the unstructured entry keeps a host
+// copy of its index list and compares it in full on every hit, so a list mutated in place gets
+// a fresh plan. Evicted or replaced plans are never freed under the lock with a device-wide
+// synchronisation: they are retired and freed once the event recorded after their last
+// execution has completed (plans executed inside a stream capture are kept: a graph may still
+// reference their device tables).
+template<typename Plan>
+struct cached_plan
 {
-    try
+    std::unique_ptr<Plan> plan;
+    std::vector<char> content;  // unstructured: the index list bytes the plan was built from
+    hipEvent_t last = nullptr;  // recorded after each execution on a non-capturing stream
+    bool captured = false;
+    ~cached_plan()
     {
-        g_error.clear();
-        return f();
+        if (last) (void)hipEventDestroy(last);
     }
-    catch (const invalid& e)
-    {
-        g_error = e.what();
-        return GHX_ERR_INVALID;
-    }
-    catch (const hip_error& e)
-    {
-        g_error = std::string(e.what()) + ": " + hipGetErrorString(hipGetLastError());
-        return GHX_ERR_HIP;
-    }
-    catch (const std::bad_alloc&)
-    {
-        g_error = "out of host memory";
-        return GHX_ERR_NOMEM;
-    }
-    catch (const std::exception& e)
-    {
-        g_error = e.what();
-        return GHX_ERR_PATTERN;
-    }
-}
+};
 
-// Plan cache for the per-field convenience entry points (ghx_structured_pack/unpack): keyed by
-// the bytes of (descriptor, iteration spaces, direction), like the reference's pattern
-// container that outlives its exchanges (include/ghex/pattern_container.hpp:84-87).
-class plan_cache
+template<typename Plan>
+class plan_lru
 {
+    using entry = std::shared_ptr<cached_plan<Plan>>;
     std::mutex mtx_;
     std::list<std::string> lru_;
-    std::unordered_map<std::string, std::pair<std::unique_ptr<splan>, std::list<std::string>::iterator>> map_;
+    std::unordered_map<std::string, std::pair<entry, std::list<std::string>::iterator>> map_;
+    std::vector<entry> retired_;
     static constexpr size_t kCap = 256;
 
-  public:
-    const splan* get(const ghx_field_desc& f, const ghx_box* boxes, int n, int dir)
+    void retire(entry e) { retired_.push_back(std::move(e)); }
+    void reap()  // free retired plans nobody holds whose last execution has completed
     {
-        std::string key(reinterpret_cast<const char*>(&f), sizeof(f));
-        key.append(reinterpret_cast<const char*>(boxes), sizeof(ghx_box) * size_t(n));
-        key.push_back(char(dir));
+        std::vector<entry> keep;
+        for (auto& e : retired_)
+        {
+            const bool idle = e.use_count() == 1 && !e->captured &&
+                              (!e->last || hipEventQuery(e->last) == hipSuccess);
+            if (!idle) keep.push_back(std::move(e));
+        }
+        retired_.swap(keep);
+    }
+
+  public:
+    // the cached entry for `key` if `same(entry)` holds, else the one `make()` builds
+    template<typename Same, typename Make>
+    entry get(const std::string& key, Same&& same, Make&& make)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mtx_);
+            auto it = map_.find(key);
+            if (it != map_.end() && same(*it->second.first))
+            {
+                lru_.splice(lru_.begin(), lru_, it->second.second);
+                return it->second.first;
+            }
+        }
+        entry fresh = make();  // plan construction (device upload) outside the lock
         std::lock_guard<std::mutex> lk(mtx_);
+        reap();
         auto it = map_.find(key);
         if (it != map_.end())
         {
-            lru_.splice(lru_.begin(), lru_, it->second.second);
-            return it->second.first.get();
+            retire(it->second.first);  // stale content (or built concurrently): replace
+            lru_.erase(it->second.second);
+            map_.erase(it);
         }
-        ghx_pack_entry e{};
-        e.field = f;
-        e.field_slot = 0;
-        e.buffer_slot = 0;
-        e.buffer_offset = 0;
-        e.boxes = boxes;
-        e.n_boxes = n;
-        auto p = std::make_unique<splan>(&e, 1, dir);
         if (map_.size() >= kCap)
         {
-            // plans of evicted keys may still be in flight on some stream: drain before freeing
-            (void)hipDeviceSynchronize();
-            map_.erase(lru_.back());
+            auto old = map_.find(lru_.back());
+            retire(old->second.first);
+            map_.erase(old);
             lru_.pop_back();
         }
         lru_.push_front(key);
-        const splan* raw = p.get();
-        map_.emplace(key, std::make_pair(std::move(p), lru_.begin()));
-        return raw;
+        map_.emplace(key, std::make_pair(fresh, lru_.begin()));
+        return fresh;
+    }
+
+    // stream-ordered record of a use (no host synchronisation)
+    void used(cached_plan<Plan>& c, void* stream)
+    {
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(s, &st);
+        std::lock_guard<std::mutex> lk(mtx_);
+        if (st != hipStreamCaptureStatusNone)
+        {
+            c.captured = true;
+            return;
+        }
+        if (!c.last && hipEventCreateWithFlags(&c.last, hipEventDisableTiming) != hipSuccess)
+        {
+            c.last = nullptr;
+            c.captured = true;  // cannot track it: never free it
+            return;
+        }
+        if (hipEventRecord(c.last, s) != hipSuccess) c.captured = true;
     }
 };
-plan_cache& cache()
+
+plan_lru<splan>& cache()
 {
-    static plan_cache c;
+    static plan_lru<splan> c;
     return c;
 }
 
-// Plan cache for ghx_unstructured_pack/unpack. Index lists can be long (10^5-10^6), so the key
-// is (descriptor, list address, length, index width, direction) plus an FNV-1a fingerprint of
-// up to 256 evenly spaced entries — the reference's pattern keeps its lid vectors alive and
-// unchanged for its lifetime (include/ghex/unstructured/pattern.hpp:53-90), which is the
-// contract here too.
-class uplan_cache
+plan_lru<uplan>& ucache()
 {
-    std::mutex mtx_;
-    std::list<std::string> lru_;
-    std::unordered_map<std::string, std::pair<std::unique_ptr<uplan>, std::list<std::string>::iterator>> map_;
-    static constexpr size_t kCap = 256;
-
-  public:
-    const uplan* get(const ghx_udata_desc& d, const void* lids, int32_t lid_bytes, int64_t n, int dir)
-    {
-        uint64_t fp = 1469598103934665603ULL;
-        const int64_t step = n > 256 ? n / 256 : 1;
-        for (int64_t i = 0; i < n; i += step)
-        {
-            const int64_t v = lid_bytes == 8 ? static_cast<const int64_t*>(lids)[i]
-                                             : static_cast<const int32_t*>(lids)[i];
-            fp = (fp ^ uint64_t(v)) * 1099511628211ULL;
-        }
-        if (n > 0)
-        {
-            const int64_t v = lid_bytes == 8 ? static_cast<const int64_t*>(lids)[n - 1]
-                                             : static_cast<const int32_t*>(lids)[n - 1];
-            fp = (fp ^ uint64_t(v)) * 1099511628211ULL;
-        }
-        std::string key(reinterpret_cast<const char*>(&d), sizeof(d));
-        const uint64_t meta[5] = {uint64_t(reinterpret_cast<uintptr_t>(lids)), uint64_t(n),
-                                  uint64_t(lid_bytes), uint64_t(dir), fp};
-        key.append(reinterpret_cast<const char*>(meta), sizeof(meta));
-        std::lock_guard<std::mutex> lk(mtx_);
-        auto it = map_.find(key);
-        if (it != map_.end())
-        {
-            lru_.splice(lru_.begin(), lru_, it->second.second);
-            return it->second.first.get();
-        }
-        std::vector<int64_t> wide;
-        const int64_t* l64 = static_cast<const int64_t*>(lids);
-        if (lid_bytes == 4)
-        {
-            wide.resize(size_t(n));
-            for (int64_t i = 0; i < n; ++i) wide[size_t(i)] = static_cast<const int32_t*>(lids)[i];
-            l64 = wide.data();
-        }
-        ghx_upack_entry e{};
-        e.data = d;
-        e.field_slot = 0;
-        e.buffer_slot = 0;
-        e.buffer_offset = 0;
-        e.lids = l64;
-        e.n_lids = n;
-        auto p = std::make_unique<uplan>(&e, 1, dir);
-        if (map_.size() >= kCap)
-        {
-            (void)hipDeviceSynchronize();  // evicted plans may still be in flight
-            map_.erase(lru_.back());
-            lru_.pop_back();
-        }
-        lru_.push_front(key);
-        const uplan* raw = p.get();
-        map_.emplace(key, std::make_pair(std::move(p), lru_.begin()));
-        return raw;
-    }
-};
-uplan_cache& ucache()
-{
-    static uplan_cache c;
+    static plan_lru<uplan> c;
     return c;
+}
+
+int run_structured(const ghx_field_desc& f, const ghx_box* boxes, int n, int dir, void* field,
+                   void* buffer, void* stream)
+{
+    std::string key(reinterpret_cast<const char*>(&f), sizeof(f));
+    key.append(reinterpret_cast<const char*>(boxes), sizeof(ghx_box) * size_t(n));
+    key.push_back(char(dir));
+    auto c = cache().get(
+        key, [](const cached_plan<splan>&) { return true; },
+        [&] {
+            ghx_pack_entry e{};
+            e.field = f;
+            e.boxes = boxes;
+            e.n_boxes = n;
+            auto p = std::make_shared<cached_plan<splan>>();
+            p->plan = std::make_unique<splan>(&e, 1, dir);
+            return p;
+        });
+    void* fp[1] = {field};
+    void* bp[1] = {buffer};
+    const int rc = c->plan->execute(fp, 1, bp, 1, stream);
+    cache().used(*c, stream);
+    return rc;
+}
+
+int run_unstructured(const ghx_udata_desc& d, const void* lids, int32_t lid_bytes, int64_t n,
+                     int dir, void* values, void* buffer, void* stream)
+{
+    std::string key(reinterpret_cast<const char*>(&d), sizeof(d));
+    const uint64_t meta[4] = {uint64_t(reinterpret_cast<uintptr_t>(lids)), uint64_t(n),
+                              uint64_t(lid_bytes), uint64_t(dir)};
+    key.append(reinterpret_cast<const char*>(meta), sizeof(meta));
+    const size_t nbytes = size_t(n) * size_t(lid_bytes);
+    auto c = ucache().get(
+        key,
+        [&](const cached_plan<uplan>& e) {
+            return e.content.size() == nbytes && std::memcmp(e.content.data(), lids, nbytes) == 0;
+        },
+        [&] {
+            std::vector<int64_t> wide;
+            const int64_t* l64 = static_cast<const int64_t*>(lids);
+            if (lid_bytes == 4)
+            {
+                wide.resize(size_t(n));
+                for (int64_t i = 0; i < n; ++i) wide[size_t(i)] = static_cast<const int32_t*>(lids)[i];
+                l64 = wide.data();
+            }
+            ghx_upack_entry e{};
+            e.data = d;
+            e.lids = l64;
+            e.n_lids = n;
+            auto p = std::make_shared<cached_plan<uplan>>();
+            p->plan = std::make_unique<uplan>(&e, 1, dir);
+            p->content.assign(static_cast<const char*>(lids), static_cast<const char*>(lids) + nbytes);
+            return p;
+        });
+    void* fp[1] = {values};
+    void* bp[1] = {buffer};
+    const int rc = c->plan->execute(fp, 1, bp, 1, stream);
+    ucache().used(*c, stream);
+    return rc;
 }
 }  // namespace
 
+namespace
+{
+thread_local std::string g_error;
+}
 void set_error(const std::string& msg) { g_error = msg; }
 const char* get_error() { return g_error.c_str(); }
 
-// ---------------------------------------------------------------------------------------------
-// exchange planner
-// ---------------------------------------------------------------------------------------------
-struct xbuffer
-{
-    int32_t first_id, second_id, rank, tag;
-    uint64_t size = 0;
-};
-
-struct exchange_plan
-{
-    std::vector<xbuffer> send, recv;
-    std::unique_ptr<splan> spack, sunpack;
-    std::unique_ptr<uplan> upack, uunpack;
-    // the fused self exchange's own pack/unpack plans when its tile size differs from the
-    // two-launch path's (g_tune.self_tile_bytes); null = use spack/sunpack
-    std::unique_ptr<splan> self_pack, self_unpack;
-    // exchanges with self AND peer messages (build_mixed): per segment of spack the unpack
-    // segment of its self message (zero = a peer message: pack only), and the unpack plan of
-    // the peer messages alone
-    device_tables mixed_comp;
-    std::unique_ptr<splan> punpack;
-    bool mixed = false;
-    int32_t n_items = 0;
-    mutable int self_ok = -1;  // lazily checked: may pack and unpack be fused (all self)?
-
-    // Every recv buffer aliases the send buffer of the same pair, and pack segment k and unpack
-    // segment k cover the same buffer bytes with the same tiling.
-    bool self_fusable() const
-    {
-        if (self_ok >= 0) return self_ok == 1;
-        bool ok = !upack && !uunpack && spack && sunpack && send.size() == recv.size();
-        for (size_t i = 0; ok && i < send.size(); ++i)
-            ok = send[i].first_id == recv[i].first_id && send[i].second_id == recv[i].second_id &&
-                 send[i].size == recv[i].size;
-        if (ok) ok = same_tiling(*spack, *sunpack);
-        self_ok = ok ? 1 : 0;
-        return ok;
-    }
-
-    // pack segment k and unpack segment k cover the same buffer bytes with the same tiling
-    static bool same_tiling(const splan& p, const splan& q)
-    {
-        bool ok = p.host_segs.size() == q.host_segs.size() && p.n_tiles == q.n_tiles;
-        for (size_t k = 0; ok && k < p.host_segs.size(); ++k)
-        {
-            const auto& a = p.host_segs[k];
-            const auto& b = q.host_segs[k];
-            ok = a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
-                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes && a.partner < 0 &&
-                 b.partner < 0;
-        }
-        return ok;
-    }
-};
 }  // namespace ghx
-
-struct ghx_exchange : ghx::exchange_plan
-{
-};
 
 // Put plan: the pack plan of the source side and the unpack plan of the target side, segment k
 // of each covering the same virtual message bytes with the same tiling (checked).
@@ -631,10 +599,8 @@ int ghx_structured_pack(const ghx_field_desc* field, const void* field_data, voi
     return guarded([&] {
         check_ptr(field, "field");
         if (n_boxes < 0 || (n_boxes > 0 && !boxes)) throw invalid("bad boxes");
-        const splan* p = cache().get(*field, boxes, n_boxes, 0);
-        void* f[1] = {const_cast<void*>(field_data)};
-        void* b[1] = {buffer};
-        return p->execute(f, 1, b, 1, stream);
+        return run_structured(*field, boxes, n_boxes, 0, const_cast<void*>(field_data), buffer,
+                              stream);
     });
 }
 
@@ -644,10 +610,8 @@ int ghx_structured_unpack(const ghx_field_desc* field, void* field_data, const v
     return guarded([&] {
         check_ptr(field, "field");
         if (n_boxes < 0 || (n_boxes > 0 && !boxes)) throw invalid("bad boxes");
-        const splan* p = cache().get(*field, boxes, n_boxes, 1);
-        void* f[1] = {field_data};
-        void* b[1] = {const_cast<void*>(buffer)};
-        return p->execute(f, 1, b, 1, stream);
+        return run_structured(*field, boxes, n_boxes, 1, field_data, const_cast<void*>(buffer),
+                              stream);
     });
 }
 
@@ -659,10 +623,8 @@ int ghx_unstructured_pack(const ghx_udata_desc* data, const void* values, void* 
         if (lid_bytes != 4 && lid_bytes != 8) throw invalid("lid_bytes must be 4 or 8");
         if (n_lids < 0 || (n_lids > 0 && !lids)) throw invalid("bad index list");
         if (n_lids == 0) return int(GHX_OK);
-        const uplan* p = ucache().get(*data, lids, lid_bytes, n_lids, 0);
-        void* f[1] = {const_cast<void*>(values)};
-        void* b[1] = {buffer};
-        return p->execute(f, 1, b, 1, stream);
+        return run_unstructured(*data, lids, lid_bytes, n_lids, 0, const_cast<void*>(values),
+                                buffer, stream);
     });
 }
 
@@ -674,10 +636,8 @@ int ghx_unstructured_unpack(const ghx_udata_desc* data, void* values, const void
         if (lid_bytes != 4 && lid_bytes != 8) throw invalid("lid_bytes must be 4 or 8");
         if (n_lids < 0 || (n_lids > 0 && !lids)) throw invalid("bad index list");
         if (n_lids == 0) return int(GHX_OK);
-        const uplan* p = ucache().get(*data, lids, lid_bytes, n_lids, 1);
-        void* f[1] = {values};
-        void* b[1] = {const_cast<void*>(buffer)};
-        return p->execute(f, 1, b, 1, stream);
+        return run_unstructured(*data, lids, lid_bytes, n_lids, 1, values,
+                                const_cast<void*>(buffer), stream);
     });
 }
 
@@ -973,7 +933,6 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
         auto ex = std::make_unique<ghx_exchange>();
         ex->n_items = n_items;
         std::vector<ghx_pack_entry> rent;              // receive entries, for build_mixed
-        std::vector<std::vector<ghx_box>> rstore;      // (their boxes)
         for (int dir = 0; dir < 2; ++dir)
         {
             const bool receive = dir == 1;
@@ -983,11 +942,12 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
             store.reserve(size_t(n_items) * 64);
             auto& bufs = receive ? ex->recv : ex->send;
             plan_direction(items, n_items, receive, bufs, sent, uent, store);
-            if (receive)
-            {
-                rent = sent;
-                rstore = std::move(store);  // moves the inner vectors: box pointers stay valid
-            }
+            // kept for per-buffer plans (ghx_exchange_split); moving the outer vector moves the
+            // inner ones, so the entries' box pointers stay valid
+            ex->box_store[dir] = std::move(store);
+            ex->entries[dir] = sent;
+            ex->uentries[dir] = uent;
+            if (receive) rent = sent;
             if (bufs.size() > GHX_MAX_SLOTS) throw invalid("more than 64 peer buffers");
             if (!sent.empty())
                 (receive ? ex->sunpack : ex->spack) =
@@ -1086,6 +1046,35 @@ int ghx_exchange_unpack(const ghx_exchange* ex, void* const* field_ptrs, int32_t
         if (rc == GHX_OK && ex->uunpack)
             rc = ex->uunpack->execute(field_ptrs, n_fields, recv_buffers, n_recv, stream);
         return rc;
+    });
+}
+
+int ghx_exchange_split(ghx_exchange* ex)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        ex->make_split();
+        return GHX_OK;
+    });
+}
+
+int ghx_exchange_pack_buffer(const ghx_exchange* ex, int32_t index, void* const* field_ptrs,
+                             int32_t n_fields, void* const* send_buffers, int32_t n_send,
+                             ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        return ex->execute_buffer(0, index, field_ptrs, n_fields, send_buffers, n_send, stream);
+    });
+}
+
+int ghx_exchange_unpack_buffer(const ghx_exchange* ex, int32_t index, void* const* field_ptrs,
+                               int32_t n_fields, void* const* recv_buffers, int32_t n_recv,
+                               ghx_stream stream)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        return ex->execute_buffer(1, index, field_ptrs, n_fields, recv_buffers, n_recv, stream);
     });
 }
 

@@ -411,7 +411,10 @@ void staged_make_pattern(int dim, const ghx_regular_domain* doms, int n, const i
                 is_pair x = ext;  // send_right: my last hl cells go to the right neighbour
                 x.lf[i] = x.ll[i] + 1 - hl;
                 x.gf[i] = x.gl[i] + 1 - hl;
-                send[i][a][right].push_back(x);
+                // hl = 0: an empty box that the right neighbour (no left halo) never receives;
+                // the reference still keys it and its tag hand-off (make_pattern.hpp:219-243)
+                // then waits for a tag message that no rank sends — dropped here
+                if (hl > 0) send[i][a][right].push_back(x);
                 is_pair y = ext;  // recv_right
                 y.lf[i] = y.ll[i] + 1;
                 y.gf[i] = y.gl[i] + 1;
@@ -424,7 +427,7 @@ void staged_make_pattern(int dim, const ghx_regular_domain* doms, int n, const i
                 is_pair x = ext;  // send_left: my first hr cells go to the left neighbour
                 x.ll[i] = x.lf[i] - 1 + hr;
                 x.gl[i] = x.gf[i] - 1 + hr;
-                send[i][a][left].push_back(x);
+                if (hr > 0) send[i][a][left].push_back(x);  // (hr = 0: as send_right above)
             }
             if (has_left)
             {

@@ -175,9 +175,10 @@ typedef struct ghx_uplan ghx_uplan;
  * stream) for ONE index list (include/ghex/unstructured/user_concepts.hpp:583-666): gather
  * values[lids[i]] (all levels, the descriptor's layout) into `buffer` / scatter back. `lids` is
  * a HOST-readable array of int32 (lid_bytes 4) or int64 (8) local indices, e.g. the pattern's
- * iteration_space::local_indices(). Plans are cached by (descriptor, list address, length, a
- * fingerprint of the entries): the list must stay unchanged while it is in use, as the
- * reference's pattern keeps it. */
+ * iteration_space::local_indices(). Plans are cached by (descriptor, list address, length); a
+ * hit compares the whole list with the copy the plan was built from, so a list changed in place
+ * gets a new plan. Replaced plans are freed once their last execution has completed (never with
+ * a device-wide synchronisation); plans executed inside a stream capture are kept alive. */
 int ghx_unstructured_pack(const ghx_udata_desc* data, const void* values, void* buffer,
                           const void* lids, int32_t lid_bytes, int64_t n_lids, ghx_stream stream);
 int ghx_unstructured_unpack(const ghx_udata_desc* data, void* values, const void* buffer,
@@ -304,6 +305,53 @@ int ghx_exchange_pack(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
                       void* const* send_buffers, int32_t n_send, ghx_stream stream);
 int ghx_exchange_unpack(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
                         void* const* recv_buffers, int32_t n_recv, ghx_stream stream);
+
+/* Per-buffer plans: ghx_exchange_split builds one pack and one unpack plan per buffer (setup
+ * time, synchronous upload); ghx_exchange_pack_buffer / ghx_exchange_unpack_buffer then enqueue
+ * the pack of send buffer `index` / the unpack of recv buffer `index` alone, with the same
+ * pointer arrays as ghx_exchange_pack/unpack. This is the reference's per-buffer packer call on
+ * the buffer's own stream (include/ghex/communication_object.hpp:568-597, packer.hpp:124-190),
+ * used to send each message as soon as its own pack is done (:611-637). */
+int ghx_exchange_split(ghx_exchange* ex);
+int ghx_exchange_pack_buffer(const ghx_exchange* ex, int32_t index, void* const* field_ptrs,
+                             int32_t n_fields, void* const* send_buffers, int32_t n_send,
+                             ghx_stream stream);
+int ghx_exchange_unpack_buffer(const ghx_exchange* ex, int32_t index, void* const* field_ptrs,
+                               int32_t n_fields, void* const* recv_buffers, int32_t n_recv,
+                               ghx_stream stream);
+
+/* ------------------------------------------------------------------------------------------
+ * RCCL transport (one rank per GPU, xGMI inside a node): replaces oomph's NCCL backend
+ * (start_group/send/recv/end_group, include/ghex/communication_object.hpp:278-281, 641-714).
+ * RCCL is loaded at run time from `path` (NULL: "librccl.so.1") — pass the library the process
+ * already uses (torch's), so one RCCL instance serves both.
+ * ------------------------------------------------------------------------------------------ */
+int ghx_rccl_open(const char* path);
+int ghx_rccl_unique_id(unsigned char id[128]);
+/* ncclCommInitRank (blocking until all `nranks` ranks have called it). */
+int ghx_rccl_comm_init(const unsigned char id[128], int32_t nranks, int32_t rank, void** comm);
+int ghx_rccl_comm_destroy(void* comm);
+/* GHX_OK, or the communicator's asynchronous error as GHX_ERR_HIP. */
+int ghx_rccl_comm_check(void* comm);
+
+/* Per-peer pipelined exchange (the reference's per-buffer streams + send-as-packed,
+ * include/ghex/device/cuda/stream.hpp:25-73, communication_object.hpp:568-637, 703-767): for
+ * each peer, in the given order, on its own greatest-priority stream: pack of its send buffers,
+ * one RCCL group {recv..., send...} on comms[k] (the peer is rank comm_ranks[k] there), unpack of
+ * its recv buffers. Messages of one pair are issued in (tag, domain pair) order on both sides.
+ * Buffers of ranks not listed must be self messages (my_rank): packed and unpacked on the
+ * caller's stream. ghx_pipeline_run enqueues all of it; the caller's stream then waits for every
+ * peer stream (no host synchronisation). Every rank must list its peers in one global order
+ * consistent across ranks (e.g. round-robin tournament rounds) so that no wait cycle can form
+ * when streams share hardware queues. Not re-entrant: one run at a time per pipeline. */
+typedef struct ghx_pipeline ghx_pipeline;
+int ghx_pipeline_create(ghx_exchange* ex, int32_t my_rank, int32_t n_peers,
+                        const int32_t* peer_ranks, void* const* comms, const int32_t* comm_ranks,
+                        ghx_pipeline** out);
+int ghx_pipeline_run(const ghx_pipeline* pl, void* const* field_ptrs, int32_t n_fields,
+                     void* const* send_buffers, int32_t n_send, void* const* recv_buffers,
+                     int32_t n_recv, ghx_stream stream);
+int ghx_pipeline_destroy(ghx_pipeline* pl);
 
 /* Self messages (a periodic wrap onto the same rank, or two domains of one rank) never leave
  * the device in the reference's stream-aware flow either (communication_object.hpp:703-767:

@@ -284,13 +284,16 @@ def staged_make_pattern(ranks_domains: Sequence[Sequence[RegularDomain]], lookup
                         box(lf[i] - hl, lf[i] - 1, gf[i] - hl, gf[i] - 1))
                 if has_right:
                     right = lookup(d.id, off_r)
-                    send.setdefault(right, []).append(
-                        box(ll[i] + 1 - hl, ll[i], gl[i] + 1 - hl, gl[i]))
+                    if hl > 0:  # hl = 0: empty, never received (the reference keys it and
+                        # its tag hand-off, make_pattern.hpp:219-243, then waits forever)
+                        send.setdefault(right, []).append(
+                            box(ll[i] + 1 - hl, ll[i], gl[i] + 1 - hl, gl[i]))
                     recv.setdefault(right, []).append(
                         box(ll[i] + 1, ll[i] + hr, gl[i] + 1, gl[i] + hr))
                 if has_left:
-                    send.setdefault(left, []).append(
-                        box(lf[i], lf[i] - 1 + hr, gf[i], gf[i] - 1 + hr))
+                    if hr > 0:  # (hr = 0: as send_right above)
+                        send.setdefault(left, []).append(
+                            box(lf[i], lf[i] - 1 + hr, gf[i], gf[i] - 1 + hr))
                     lf[i] -= hl
                     gf[i] -= hl
                 if has_right:

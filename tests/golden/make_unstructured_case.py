@@ -6,6 +6,7 @@ Holds the reference's own known-answer unstructured test data:
   * test/bindings/python/test_unstructured_domain_descriptor.py:45-213 (4 domains with repeated
     halo gids and self-exchange) — the `domains = {...}` literal is read from the file as data.
 """
+import ast
 import json
 import os
 
@@ -35,10 +36,11 @@ case = {
 if __name__ == "__main__":
     src = open(REF_PY).read()
     body = src[src.index("domains = {"):src.index("# fmt: on")]
-    ns = {}
-    exec(body, ns)  # a dict literal of integers (data only)
+    # the text after "domains = " is a dict literal of integers: parsed as data, never executed
+    literal = body[body.index("{"):].strip()
+    domains = ast.literal_eval(literal)
     py = {str(k): {kk: v[kk] for kk in ("all", "outer", "outer_lids", "inner")}
-          for k, v in ns["domains"].items()}
+          for k, v in domains.items()}
     case["python_fixture"] = {
         "source": "test/bindings/python/test_unstructured_domain_descriptor.py:45-213, LEVELS=2",
         "levels": 2, "value_encoding": "rank*1000 + 10*gid + level", "domains": py}

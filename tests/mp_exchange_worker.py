@@ -6,9 +6,10 @@ MASTER_ADDR / MASTER_PORT in the environment; exits 0 when every cell of the ran
 
 With mode "bulk" the exchange is the zero-copy BulkCommunicationObject instead: every rank puts
 its send regions straight into the peers' fields through IPC mappings (same GPU here, peer
-GPUs over xGMI on a multi-GPU node).
+GPUs over xGMI on a multi-GPU node). Mode "pipe" is the pipelined host-staged exchange (one
+stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk|sched]"""
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk|sched|pipe]"""
 import os
 import sys
 
@@ -56,6 +57,10 @@ def main():
                 h.schedule_wait(s)
                 assert co.has_scheduled_exchange()
                 h.wait()
+        elif mode == "pipe":  # per-peer streams: pack -> D2H -> send as landed -> H2D -> unpack
+            co = R.make_communication_object(ctx, staging="host", pipelined=True)
+            for _ in range(reps):
+                co.exchange([pc(fd)]).wait()
         else:
             co = R.make_communication_object(ctx, staging="host")
             for _ in range(reps):

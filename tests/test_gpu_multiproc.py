@@ -27,10 +27,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("mode", ["staged", "bulk", "sched"])
-@pytest.mark.parametrize("parts,N,Hw", [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)])
-def test_exchange_multi_process(parts, N, Hw, mode):
-    """staged: CommunicationObject(staging="host") over gloo; bulk: zero-copy IPC puts."""
+def _run(parts, N, Hw, mode):
     world = parts[0] * parts[1] * parts[2]
     port = _free_port()
     procs = []
@@ -53,3 +50,17 @@ def test_exchange_multi_process(parts, N, Hw, mode):
         codes.append(p.returncode)
     assert codes == [0] * world, "\n".join(outs)
     assert "bad cells 0" in outs[0]
+
+
+@pytest.mark.parametrize("mode", ["staged", "bulk", "sched", "pipe"])
+@pytest.mark.parametrize("parts,N,Hw", [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)])
+def test_exchange_multi_process(parts, N, Hw, mode):
+    """staged: CommunicationObject(staging="host") over gloo; bulk: zero-copy IPC puts; pipe:
+    the pipelined host-staged exchange (per-peer streams, send as each copy lands)."""
+    _run(parts, N, Hw, mode)
+
+
+def test_pipelined_eight_ranks():
+    """The 2x2x2 decomposition (7 peers per rank, every pair once in the round order) with the
+    pipelined host-staged exchange, 8 processes on the one GPU."""
+    _run((2, 2, 2), 8, 2, "pipe")

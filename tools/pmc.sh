@@ -10,5 +10,5 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace -d $OUT/p$i -o pmc --output-format csv -- python3 $R/bench.py --no-graph --no-extras --no-cpu-baseline "$@" > $OUT/p$i.log 2>&1
+  timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace -d $OUT/p$i -o pmc --output-format csv -- python3 $R/bench.py --no-graph --no-extras --no-cpu-baseline --no-cold "$@" > $OUT/p$i.log 2>&1
 done

@@ -10,19 +10,19 @@ OUT=$R/gpurun_out/prof_$RN
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 if [ "${PMC_ONLY:-0}" != 1 ]; then
-# 1) the bench command itself (defaults: N=1, 512^3, H=2, hipGraph, extras, cpu baseline)
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/bench -o kt --output-format csv -- python3 $R/bench.py > $OUT/bench.log 2>&1
+# 1) the bench command itself (defaults: N=1, 512^3, H=2, hipGraph, extras, cpu baseline) minus
+#    the cold-cache legs, whose extra launches of the same kernels would skew the averages
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/bench -o kt --output-format csv -- python3 $R/bench.py --no-cold > $OUT/bench.log 2>&1
 # 2) kernel traces at halo 1 and 3
 for h in 1 3; do
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/h$h -o kt --output-format csv -- python3 $R/bench.py --halo $h --no-extras --no-cpu-baseline > $OUT/h$h.log 2>&1
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/h$h -o kt --output-format csv -- python3 $R/bench.py --halo $h --no-extras --no-cpu-baseline --no-cold > $OUT/h$h.log 2>&1
 done
 fi
 # 3) PMC passes (one counter group per pass, kernel trace only), eager launches: the two-launch
-#    pack/unpack path at halo 1/2/3, and the fused self-exchange kernel the N=1 bench runs at 2
+#    pack/unpack path at halo 1/2/3 (the fused k_self of the extras is counted too)
 if [ "${SKIP_PMC:-0}" != 1 ]; then
   for h in 1 2 3; do
-    bash $R/tools/pmc.sh $OUT/pmc_h$h --steps 20 --warmup 5 --halo $h --unfused
+    bash $R/tools/pmc.sh $OUT/pmc_h$h --steps 20 --warmup 5 --halo $h
   done
-  bash $R/tools/pmc.sh $OUT/pmc_h2_self --steps 20 --warmup 5 --halo 2
 fi
 echo done > $OUT/DONE
