@@ -7,8 +7,10 @@ T=${1:-c}
 O=gpurun_out/$T
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread \
-  > $O/tests.log 2>&1; echo "tests rc=$?" >> $O/status
+  > $O/tests.log 2>&1; rc=$?; echo "tests rc=$rc" >> $O/status
 tail -3 $O/tests.log
+# 0 = passed, 1 = some tests failed: go on; anything else (timeout, abort, fault): stop here
+if [ $rc -gt 1 ]; then cat $O/status; exit $rc; fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_20_5.json 2> $O/bench_20_5.err \
   && timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err \
   && timeout -k 10 600 bash tools/rehearse_multi.sh $O/rehearse
