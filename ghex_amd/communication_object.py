@@ -535,19 +535,17 @@ class CommunicationObject:
                 x = plan.send[i]
                 sops.append(dist.isend(hs[i][:x["size"]], self.context.global_rank(p), group,
                                        x["tag"]))
-        while rops:
-            for op in list(rops):
-                w, j, p = op
-                if not w.is_completed():
-                    continue
-                w.wait()
-                rops.remove(op)
-                sp = self._peer_stream(p, device)
-                n = plan.recv[j]["size"]
-                with torch.cuda.stream(sp):
-                    recv[j][:n].copy_(hr[j][:n], non_blocking=True)
-                _ghx.check(L.ghx_exchange_unpack_buffer(plan.h, j, fptrs, nf, rptrs, len(recv),
-                                                        sp.cuda_stream), "unpack_buffer")
+        # every send is posted before the first blocking receive wait, so the in-order waits
+        # below cannot deadlock; each message's H2D + unpack is queued as soon as it is in (gloo
+        # receive works complete only inside wait(): no polling)
+        for w, j, p in rops:
+            w.wait()
+            sp = self._peer_stream(p, device)
+            n = plan.recv[j]["size"]
+            with torch.cuda.stream(sp):
+                recv[j][:n].copy_(hr[j][:n], non_blocking=True)
+            _ghx.check(L.ghx_exchange_unpack_buffer(plan.h, j, fptrs, nf, rptrs, len(recv),
+                                                    sp.cuda_stream), "unpack_buffer")
         for w in sops:
             w.wait()
         for p in peers:

@@ -41,7 +41,7 @@ def _run(parts, N, Hw, mode):
     outs, codes = [], []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=240)
+            out, _ = p.communicate(timeout=120)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()

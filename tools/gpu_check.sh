@@ -6,7 +6,7 @@ set -o pipefail
 T=${1:-c}
 O=gpurun_out/$T
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
   > $O/tests.log 2>&1; rc=$?; echo "tests rc=$rc" >> $O/status
 tail -3 $O/tests.log
 # 0 = passed, 1 = some tests failed: go on; anything else (timeout, abort, fault): stop here
