@@ -469,7 +469,7 @@ int ghx_tune(const char* key, int32_t value)
         }
         else if (k == "pair")
         {
-            if (value < 0 || value > 1) throw invalid("pair must be 0 or 1");
+            if (value < 0 || value > 2) throw invalid("pair must be 0, 1 or 2");
             g_tune.pair = value;
         }
         else if (k == "self_tile_bytes")

@@ -43,9 +43,11 @@ struct tuning
                                        // segments first, 2 round-robin over segments
     int pair = 0;                      // pair short-row segments whose rows interleave in
                                        // memory (the +x face of row y and the -x face of row
-                                       // y+1 share a cache line): one lane moves both. Off by
-                                       // default: with short-row-first dispatch the L2 already
-                                       // merges the shared-line misses (same TCC_EA0_RDREQ)
+                                       // y+1 share a cache line): 1 one lane moves both, 2 the
+                                       // two rows of a line go to adjacent lanes of one wave
+                                       // instruction (copy_tile_ilv). 1 is off by default: with
+                                       // short-row-first dispatch the L2 already merges the
+                                       // shared-line misses (same TCC_EA0_RDREQ)
     int urun = 1;                      // unstructured 4/8-B-row segments: 16-B lane chunks with
                                        // run detection (copy_runs)
     uint32_t u_run_tile_rows = 2048;   // rows per tile of run-heavy index-list segments
@@ -174,7 +176,7 @@ void set_error(const std::string& msg);
 const char* get_error();
 
 // kernel launchers (ghx_kernels.hip)
-int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid, bool pairs);
+int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid, int pairs);
 int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid, bool runs);
 int launch_self(const kargs& a, void* stream, uint32_t grid);
 int launch_put(const kargs& a, void* stream, uint32_t grid);

@@ -480,6 +480,54 @@ __device__ __forceinline__ void copy_tile_pair(const seg_s& s, const seg_s& q,
     }
 }
 
+// Interleaved pairs (knob pair = 2): the rows of the primary P and of its line partner Q (row r
+// of P shares a cache line with row r-1 of Q: the -x piece of row y+1 and the +x piece of row y
+// of a unit-stride field) are dealt to ALTERNATE lanes — lane 2i moves row i of P, lane 2i+1
+// row i-1 of Q — so the two pieces of one line are requested by ONE wave instruction, which the
+// texture addresser merges into one request per line (per-lane pairing issues them in two
+// instructions). Each buffer side stays a contiguous stream (even lanes into P's range, odd
+// lanes into Q's). Rows of exactly one vector (L == W: 8 or 16 B, halo 1 or 2 of fp64).
+template<bool PACK, int W, int U, int NT>
+__device__ __forceinline__ void copy_tile_ilv(const seg_s& s, const seg_s& q,
+                                              char* __restrict__ field, char* __restrict__ buf,
+                                              char* __restrict__ qbuf, uint32_t start,
+                                              uint32_t end)
+{
+    using V = typename vec_t<W>::type;
+    constexpr bool NTL = NT >= 2;
+    constexpr bool NTS = NT == 1 || NT == 2;
+    const uint32_t total = 2 * ((end - start) / W);  // whole rows per tile (planner)
+    for (uint32_t e0 = threadIdx.x; e0 < total; e0 += U * kBlock)
+    {
+        V v[U];
+        int64_t fo[U];
+        char* bp[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t e = e0 + uint32_t(u) * kBlock;
+            const uint32_t side = e & 1u;
+            const uint32_t p = start + (e >> 1) * W;  // primary row position
+            ok[u] = e < total && (side == 0 || p >= W);
+            const uint32_t pp = side ? p - W : p;
+            // P and Q have the same shape: only their bases differ
+            fo[u] = field_offset_s(s, pp) - s.field_off + (side ? q.field_off : s.field_off);
+            bp[u] = (side ? qbuf : buf) + pp;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (ok[u]) v[u] = PACK ? vload<V, NTL>(field + fo[u]) : vload<V, NTL>(bp[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (ok[u])
+            {
+                if (PACK) vstore<V, NTS>(bp[u], v[u]);
+                else vstore<V, NTS>(field + fo[u], v[u]);
+            }
+    }
+}
+
 template<bool PACK, int U, int NT>
 __device__ __forceinline__ void dispatch_pair(const seg_s& s, const seg_s& q, char* field,
                                               char* buf, char* qbuf, uint32_t start, uint32_t end,
@@ -495,14 +543,14 @@ __device__ __forceinline__ void dispatch_pair(const seg_s& s, const seg_s& q, ch
     }
 }
 
-template<bool PACK, int U, int NT, typename Seg>
+template<bool PACK, int U, int NT, bool ILV, typename Seg>
 __device__ __forceinline__ bool try_pair(const Seg&, const Seg*, const kargs&, char*, char*,
                                          uint32_t, uint32_t, int)
 {
     return false;
 }
 
-template<bool PACK, int U, int NT>
+template<bool PACK, int U, int NT, bool ILV>
 __device__ __forceinline__ bool try_pair(const seg_s& s, const seg_s* segs, const kargs& a,
                                          char* field, char* buf, uint32_t start, uint32_t end,
                                          int w)
@@ -511,6 +559,19 @@ __device__ __forceinline__ bool try_pair(const seg_s& s, const seg_s* segs, cons
     const seg_s q = segs[s.partner];
     char* qbuf = reinterpret_cast<char*>(a.buf_ptr[q.buf_slot]) + q.buf_off;
     w = min(w, int(__builtin_ctzll(reinterpret_cast<uint64_t>(qbuf) | 16ull)));
+    if constexpr (ILV)
+    {
+        if (w == 4 && s.row_bytes == 16)
+        {
+            copy_tile_ilv<PACK, 16, U, NT>(s, q, field, buf, qbuf, start, end);
+            return true;
+        }
+        if (w == 3 && s.row_bytes == 8)
+        {
+            copy_tile_ilv<PACK, 8, U, NT>(s, q, field, buf, qbuf, start, end);
+            return true;
+        }
+    }
     dispatch_pair<PACK, U, NT>(s, q, field, buf, qbuf, start, end, w);
     return true;
 }
@@ -525,7 +586,8 @@ __device__ __forceinline__ int ptr_wlog2(uint64_t p)
 // general path's registers do not weigh on it and vice versa. PAIR (structured only): the plan
 // holds paired segments (knob "pair"); the pair path more than doubles the kernel's VGPRs
 // (156 vs 73 at U=4), so plans without pairs launch the variant that leaves it out.
-template<bool PACK, int U, int NT, typename Seg, bool RUNS = false, bool PAIR = false>
+template<bool PACK, int U, int NT, typename Seg, bool RUNS = false, bool PAIR = false,
+         bool ILV = false>
 __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
 {
     const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
@@ -549,7 +611,7 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         }
         if constexpr (PAIR)
         {
-            if (try_pair<PACK, U, NT>(s, segs, a, field, buf, start, end, w)) continue;
+            if (try_pair<PACK, U, NT, ILV>(s, segs, a, field, buf, start, end, w)) continue;
         }
         switch (w)
         {
@@ -869,12 +931,17 @@ uint32_t grid_for_tiles(uint32_t n_tiles)
     return n_tiles < cap ? n_tiles : cap;
 }
 
-int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid, bool pairs)
+int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid, int pairs)
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    // plans with paired segments (a developer knob): one variant, U = 4, default cache policy
-    if (pairs && direction == 0)
+    // plans with paired segments (knob "pair"): one variant, U = 4, default cache policy;
+    // pairs == 2: the two rows of a line on alternate lanes of one instruction
+    if (pairs == 2 && direction == 0)
+        hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (pairs == 2)
+        hipLaunchKernelGGL((k_copy<false, 4, 0, seg_s, false, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (pairs && direction == 0)
         hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (pairs)
         hipLaunchKernelGGL((k_copy<false, 4, 0, seg_s, false, true>), dim3(grid), dim3(kBlock), 0, s, a);

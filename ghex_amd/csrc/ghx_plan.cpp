@@ -439,7 +439,8 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
     std::vector<uint32_t> tiles = build_tiles(segs, g_tune.pair ? &consumed : nullptr);
     n_segments = int32_t(segs.size());
     n_tiles = uint32_t(tiles.size() / 2);
-    for (const seg_s& s : segs) has_pairs = has_pairs || s.partner >= 0;
+    for (const seg_s& s : segs)
+        if (s.partner >= 0) has_pairs = g_tune.pair == 2 ? 2 : 1;
     host_segs = segs;
     upload(dev, segs, tiles);
 }

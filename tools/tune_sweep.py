@@ -62,8 +62,25 @@ def main():
         tp = sorted(e[0].elapsed_time(e[1]) for e in ev)[a.iters // 2] * 1e3
         tu = sorted(e[1].elapsed_time(e[2]) for e in ev)[a.iters // 2] * 1e3
         nbytes = (E ** 3 - N ** 3) * 8
+        # the bench's form: hipGraphs of 10 (pack, unpack) steps, 20 replays, device time
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            gs = torch.cuda.current_stream().cuda_stream
+            for _ in range(10):
+                L.ghx_exchange_pack(plan.h, fp, 1, sp, len(send), gs)
+                L.ghx_exchange_unpack(plan.h, fp, 1, rp, len(recv), gs)
+        g.replay()
+        torch.cuda.synchronize()
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0.record()
+        for _ in range(20):
+            g.replay()
+        g1.record()
+        torch.cuda.synchronize()
+        tg = g0.elapsed_time(g1) * 1e3 / 200
         out.append(dict(cfg=cfg, pack_us=round(tp, 2), unpack_us=round(tu, 2),
-                        step_GBps=round(4 * nbytes / (tp + tu) / 1e3, 1)))
+                        step_GBps=round(4 * nbytes / (tp + tu) / 1e3, 1),
+                        graph_step_us=round(tg, 2), graph_GBps=round(4 * nbytes / tg / 1e3, 1)))
         print(json.dumps(out[-1]), flush=True)
         del co, plan
 
