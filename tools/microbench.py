@@ -54,6 +54,9 @@ def main():
     for i, b in enumerate(send):
         groups.setdefault(cls(b), []).append(i)
     groups["all"] = list(range(len(send)))
+    # short rows (x extent <= H: the request-bound part) vs long rows (streaming)
+    groups["short_rows"] = [i for i, b in enumerate(send) if b[1][0] - b[0][0] + 1 <= H]
+    groups["long_rows"] = [i for i, b in enumerate(send) if b[1][0] - b[0][0] + 1 > H]
 
     def plan(boxes, direction):
         arr = (_ghx.Box * len(boxes))()
