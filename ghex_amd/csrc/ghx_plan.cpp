@@ -115,13 +115,14 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
     {
         std::vector<uint32_t> idx(segs.size());
         for (uint32_t i = 0; i < segs.size(); ++i) idx[i] = i;
-        if (g_tune.order == 1)
+        if (g_tune.order == 1 || g_tune.order == 3)
             std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
                 return (segs[a].row_bytes < g_tune.small_row_bytes) >
                        (segs[b].row_bytes < g_tune.small_row_bytes);
             });
         std::vector<int32_t> partner(segs.size(), -1);
-        if (g_tune.order == 1 && g_tune.xcd_pair && !g_tune.pair) partner = line_partners(segs);
+        if ((g_tune.order == 1 || g_tune.order == 3) && g_tune.xcd_pair && !g_tune.pair)
+            partner = line_partners(segs);
         // Line-sharing pairs first, in lock-step groups of 8 tiles: tile t of one half at block
         // 16k + i, tile t of the other at 16k + 8 + i -> the same XCD (blocks are dealt
         // round-robin over the 8 XCDs) at about the same time, so each shared line is fetched
@@ -152,6 +153,40 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
             }
         }
         for (; next < rest.size(); ++next) emit(rest[next].first, rest[next].second);
+        if (g_tune.order == 3)
+        {
+            // spread: the short-row units (16 consecutive blocks, so lock-step pair groups stay
+            // aligned) dealt evenly among the long-row units instead of all first, so that every
+            // stretch of the launch mixes request-bound and streaming tiles
+            const size_t nt = out.size() / 2, U = 16;
+            std::vector<std::pair<size_t, size_t>> sh, lo;  // [first tile, end tile)
+            for (size_t t = 0; t < nt; t += U)
+            {
+                const size_t e = std::min(nt, t + U);
+                bool any_short = false;
+                for (size_t k = t; k < e; ++k)
+                    any_short = any_short || segs[out[2 * k]].row_bytes < g_tune.small_row_bytes;
+                (any_short ? sh : lo).emplace_back(t, e);
+            }
+            std::vector<uint32_t> spread;
+            spread.reserve(out.size());
+            auto put = [&](std::pair<size_t, size_t> u) {
+                for (size_t k = u.first; k < u.second; ++k)
+                {
+                    spread.push_back(out[2 * k]);
+                    spread.push_back(out[2 * k + 1]);
+                }
+            };
+            size_t li = 0;
+            for (size_t si = 0; si < sh.size(); ++si)
+            {
+                const size_t upto = (si * lo.size()) / std::max<size_t>(1, sh.size());
+                for (; li < upto; ++li) put(lo[li]);
+                put(sh[si]);
+            }
+            for (; li < lo.size(); ++li) put(lo[li]);
+            out.swap(spread);
+        }
     }
     return out;
 }

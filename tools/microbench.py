@@ -101,6 +101,35 @@ def main():
                 "us": round(us, 2), "bytes": nb, "tiles": nt,
                 "GBps_alg": round(2 * nb / us / 1e3, 1)}
             L.ghx_plan_destroy(h)
+    # short-row and long-row spaces as two launches on two streams at once (does the hardware
+    # overlap them better than one launch that holds both?)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+    for direction, boxes in ((0, send), (1, recv)):
+        hs, _, _ = plan([boxes[i] for i in groups["short_rows"]], direction)
+        hl, _, _ = plan([boxes[i] for i in groups["long_rows"]], direction)
+
+        def both():
+            sa.wait_stream(main)
+            sb.wait_stream(main)
+            L.ghx_plan_execute(hs, fp, 1, bp, 1, sa.cuda_stream)
+            L.ghx_plan_execute(hl, fp, 1, bp, 1, sb.cuda_stream)
+            main.wait_stream(sa)
+            main.wait_stream(sb)
+        for _ in range(5):
+            both()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(a.iters)]
+        for e0, e1 in ev:
+            e0.record()
+            both()
+            e1.record()
+        torch.cuda.synchronize()
+        ts = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
+        res[f"short_long_two_streams_{'pack' if direction == 0 else 'unpack'}"] = {
+            "us": round(ts[len(ts) // 2] * 1e3, 2)}
+        L.ghx_plan_destroy(hs)
+        L.ghx_plan_destroy(hl)
     # plain copies for reference
     for mb in (25, 50, 100, 400):
         nbytes = mb * 1024 * 1024
