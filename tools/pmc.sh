@@ -4,7 +4,7 @@
 # Usage: tools/pmc.sh <outdir> [bench args...]
 set -e
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$1; shift
+OUT=$(realpath -m "$1"); shift
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 i=0

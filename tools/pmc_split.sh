@@ -4,7 +4,7 @@
 # trace only. Rows are told apart by their grid (workgroup count). Usage: tools/pmc_split.sh <out>
 set -e
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$1; shift
+OUT=$(realpath -m "$1"); shift
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 i=0
