@@ -464,7 +464,7 @@ int ghx_tune(const char* key, int32_t value)
         }
         else if (k == "order")
         {
-            if (value < 0 || value > 3) throw invalid("order must be 0, 1, 2 or 3");
+            if (value < 0 || value > 4) throw invalid("order must be in 0..4");
             g_tune.order = value;
         }
         else if (k == "pair")

@@ -41,7 +41,8 @@ struct tuning
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
     int order = 1;                     // tile dispatch order: 0 segment order, 1 short-row
                                        // segments first, 2 round-robin over segments, 3 the
-                                       // short-row units spread evenly among the long ones
+                                       // short-row units spread evenly among the long ones,
+                                       // 4 short-row units last
     int pair = 0;                      // pair short-row segments whose rows interleave in
                                        // memory (the +x face of row y and the -x face of row
                                        // y+1 share a cache line): 1 one lane moves both, 2 the

@@ -115,13 +115,13 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
     {
         std::vector<uint32_t> idx(segs.size());
         for (uint32_t i = 0; i < segs.size(); ++i) idx[i] = i;
-        if (g_tune.order == 1 || g_tune.order == 3)
+        if (g_tune.order == 1 || g_tune.order >= 3)
             std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
                 return (segs[a].row_bytes < g_tune.small_row_bytes) >
                        (segs[b].row_bytes < g_tune.small_row_bytes);
             });
         std::vector<int32_t> partner(segs.size(), -1);
-        if ((g_tune.order == 1 || g_tune.order == 3) && g_tune.xcd_pair && !g_tune.pair)
+        if ((g_tune.order == 1 || g_tune.order >= 3) && g_tune.xcd_pair && !g_tune.pair)
             partner = line_partners(segs);
         // Line-sharing pairs first, in lock-step groups of 8 tiles: tile t of one half at block
         // 16k + i, tile t of the other at 16k + 8 + i -> the same XCD (blocks are dealt
@@ -153,6 +153,23 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
             }
         }
         for (; next < rest.size(); ++next) emit(rest[next].first, rest[next].second);
+        if (g_tune.order == 4)
+        {
+            // long-row units first, the short-row units (16-block groups) after them
+            const size_t nt = out.size() / 2, U = 16;
+            std::vector<uint32_t> sh, lo;
+            for (size_t t = 0; t < nt; t += U)
+            {
+                const size_t e = std::min(nt, t + U);
+                bool any_short = false;
+                for (size_t k = t; k < e; ++k)
+                    any_short = any_short || segs[out[2 * k]].row_bytes < g_tune.small_row_bytes;
+                auto& dst = any_short ? sh : lo;
+                dst.insert(dst.end(), out.begin() + std::ptrdiff_t(2 * t), out.begin() + std::ptrdiff_t(2 * e));
+            }
+            lo.insert(lo.end(), sh.begin(), sh.end());
+            out.swap(lo);
+        }
         if (g_tune.order == 3)
         {
             // spread: the short-row units (16 consecutive blocks, so lock-step pair groups stay

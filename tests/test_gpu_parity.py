@@ -383,6 +383,7 @@ def test_full_size_512_h2_checksum():
 
 @pytest.mark.parametrize("knobs", [{"pair": 1}, {"pair": 1, "small_tile_rows": 64},
                                    {"pair": 2}, {"pair": 2, "small_tile_rows": 64},
+                                   {"order": 3, "small_tile_rows": 512}, {"order": 4},
                                    {"order": 0, "small_tile_rows": 100, "unroll": 2},
                                    {"order": 2, "tile_bytes": 1024, "unroll": 8, "nt": 3},
                                    {"grid_cap": 7, "nt": 1}, {"short_pol": 3},
