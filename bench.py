@@ -345,7 +345,12 @@ def main():
     # pack, and of M steps + one pack + one unpack, replayed in interleaved rounds (medians);
     # pack = T1 - T0, unpack = T2 - T1.
     t_pack, t_unpack = kernel_durations(torch, dev, stream, [pack, unpack])
-    dom_name, dom_t = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+    dom_name, dom_d = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+    # the dominant launch's share of the timed region's device time (HIP events around the K
+    # steps on the launch stream), split by the live differential durations: conservative (the
+    # step's inter-launch gaps are charged to the launches), and within a few % of the rocprofv3
+    # kernel-trace mean of the same launches (profiles/r02_bench_kernels_by_grid.csv)
+    dom_t = dev_step * dom_d / (t_pack + t_unpack)
     launch_bytes = 2 * n_halo * 8  # read n*s + write n*s, either kernel
     achieved = launch_bytes / dom_t / 1e9
     traffic, traffic_src = None, None
@@ -367,8 +372,10 @@ def main():
         "traffic_source": traffic_src,
         "algorithmic_bytes_per_launch": launch_bytes,
         "launch_us": round(dom_t * 1e6, 2),
-        "launch_us_source": "HIP events on the launch stream: graphs of M steps vs M steps + "
-                            "one more launch, replayed interleaved, median difference",
+        "launch_us_source": "HIP events on the launch stream around the K timed steps: device "
+                            "time per step x the kernel's share of the step (pack_us, "
+                            "unpack_us: graphs of M steps vs M steps + one more launch, "
+                            "replayed interleaved, median differences)",
         "pack_us": round(t_pack * 1e6, 2), "unpack_us": round(t_unpack * 1e6, 2),
         "step_device_us": round(dev_step * 1e6, 2),
         "step_achieved": round(step_bytes / dev_step / 1e9, 1),

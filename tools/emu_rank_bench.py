@@ -103,7 +103,74 @@ def main():
                               "self_bytes": sum(b["size"] for b in plan.recv if b["rank"] == 0),
                               "us_per_step": round(t * 1e6, 2),
                               "GBps_per_gpu": round(4 * n_halo * 8 / t / 1e9, 1)}), flush=True)
+        if world > 1:
+            timeline(torch, dev, co, plan, send, recv, fp, sp, rp, L, _ghx, world, parts)
         del co, plan, send, recv
+
+
+def timeline(torch, dev, co, plan, send, recv, fp, sp, rp, L, _ghx, world, parts):
+    """The pipeline's on-device timeline without the transport: every peer's buffers packed on
+    its own stream (round order, as ghx_pipeline_run issues them), then every peer's buffers
+    unpacked on its stream; per peer, the time from the common start event to its pack (and
+    unpack) completing, medians over repetitions. Feeds the overlap model of DESIGN §5.1."""
+    from ghex_amd.communication_object import peer_order
+    co._split(plan)
+    peers = peer_order(0, sorted({x["rank"] for x in plan.send} - {0}), world)
+    streams = {p: torch.cuda.Stream(dev, priority=-1) for p in peers}
+    main = torch.cuda.current_stream(dev)
+    res = {p: {"pack": [], "unpack": []} for p in peers}
+    alone = {}
+    for p in peers:  # each peer's pack alone (nothing concurrent)
+        ts = []
+        for _ in range(20):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main)
+            for i, x in enumerate(plan.send):
+                if x["rank"] == p:
+                    L.ghx_exchange_pack_buffer(plan.h, i, fp, 1, sp, len(send), main.cuda_stream)
+            e1.record(main)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        alone[p] = sorted(ts)[10]
+    for rep in range(25):
+        start = torch.cuda.Event(enable_timing=True)
+        start.record(main)
+        done = {}
+        for p in peers:
+            s = streams[p]
+            s.wait_event(start)
+            for i, x in enumerate(plan.send):
+                if x["rank"] == p:
+                    L.ghx_exchange_pack_buffer(plan.h, i, fp, 1, sp, len(send), s.cuda_stream)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(s)
+            done[p] = e
+        mid = torch.cuda.Event(enable_timing=True)
+        for p in peers:
+            main.wait_stream(streams[p])
+        mid.record(main)
+        udone = {}
+        for p in peers:
+            s = streams[p]
+            s.wait_event(mid)
+            for j, x in enumerate(plan.recv):
+                if x["rank"] == p:
+                    L.ghx_exchange_unpack_buffer(plan.h, j, fp, 1, rp, len(recv), s.cuda_stream)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(s)
+            udone[p] = e
+        for p in peers:
+            main.wait_stream(streams[p])
+        torch.cuda.synchronize(dev)
+        if rep >= 5:
+            for p in peers:
+                res[p]["pack"].append(start.elapsed_time(done[p]) * 1e3)
+                res[p]["unpack"].append(mid.elapsed_time(udone[p]) * 1e3)
+    med = lambda v: round(sorted(v)[len(v) // 2], 2)  # noqa: E731
+    print(json.dumps({"world": world, "decomposition": parts, "timeline": [
+        {"peer": p, "bytes": sum(x["size"] for x in plan.send if x["rank"] == p),
+         "pack_alone_us": round(alone[p], 2), "pack_done_us": med(res[p]["pack"]),
+         "unpack_done_us": med(res[p]["unpack"])} for p in peers]}), flush=True)
 
 
 if __name__ == "__main__":
