@@ -102,7 +102,8 @@ _SIGS = {
     "ghx_rccl_comm_init": (c_i32, [P(ctypes.c_ubyte), c_i32, c_i32, P(c_vp)]),
     "ghx_rccl_comm_destroy": (c_i32, [c_vp]),
     "ghx_rccl_comm_check": (c_i32, [c_vp]),
-    "ghx_pipeline_create": (c_i32, [c_vp, c_i32, c_i32, P(c_i32), P(c_vp), P(c_i32), P(c_vp)]),
+    "ghx_pipeline_create": (c_i32, [c_vp, c_i32, c_i32, P(c_i32), P(c_vp), P(c_i32), c_i32,
+                                    P(c_vp)]),
     "ghx_pipeline_run": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
     "ghx_pipeline_destroy": (c_i32, [c_vp]),
     "ghx_unstructured_pack": (c_i32, [P(UDataDesc), c_vp, c_vp, c_vp, c_i32, ctypes.c_int64, c_vp]),

@@ -21,8 +21,9 @@ Self messages stay on the device exactly as in the default mode.
 
 pipelined=True (the reference's per-buffer streams + send-as-packed,
 include/ghex/device/cuda/stream.hpp:25-73, communication_object.hpp:568-637, 703-767): each peer
-rank gets its own greatest-priority stream on which its send buffers are packed (one launch per
-buffer), its messages exchanged and its recv buffers unpacked, so a message leaves as soon as its
+rank rides one of `max_streams` greatest-priority streams (dealt in round order; the device has
+few hardware queues) on which its send buffers are packed (one launch per buffer), its messages
+exchanged and its recv buffers unpacked, so a message leaves as soon as its
 own pack is done and is unpacked as soon as it lands. Device buffers: the native pipeline
 (ghx_pipeline_*) with one 2-rank RCCL communicator per peer pair (one shared communicator would
 serialise the per-peer groups); host staging: per-peer D2H after the pack, host sends as the
@@ -172,7 +173,7 @@ class CommunicationObject:
     """communication_object<grid, domain_id> (make_communication_object, :1105-1112)."""
 
     def __init__(self, context, fuse_self: bool = True, staging=None, pipelined: bool = False,
-                 rccl_self: bool = False):
+                 rccl_self: bool = False, max_streams: int = 4):
         if staging not in (None, "host"):
             raise ValueError("staging must be None (device buffers) or 'host'")
         self.context = context
@@ -182,6 +183,8 @@ class CommunicationObject:
         # tests: route the self messages through RCCL too (a 1-rank communicator), so the
         # pipeline's RCCL path runs on a one-GPU box
         self.rccl_self = rccl_self
+        # pipelined: peers dealt over this many streams in round order (hardware queues are few)
+        self.max_streams = max(1, int(max_streams))
         self._streams = {}
         self._comms = {}
         self._plans = {}
@@ -415,9 +418,9 @@ class CommunicationObject:
             w.wait()
 
     # -- pipelined exchange ---------------------------------------------------------------------
-    def _peer_stream(self, peer, device):
+    def _peer_stream(self, lane, device):
         import torch
-        key = (peer, str(device))
+        key = (lane, str(device))
         s = self._streams.get(key)
         if s is None:
             s = self._streams[key] = torch.cuda.Stream(device, priority=-1)
@@ -469,7 +472,7 @@ class CommunicationObject:
             h = ctypes.c_void_p()
             _ghx.call("ghx_pipeline_create", plan.h, me, len(peers), _ghx.i32_array(peers),
                       _ghx.ptr_array([c.value for c, _ in comms]),
-                      _ghx.i32_array([r for _, r in comms]), ctypes.byref(h))
+                      _ghx.i32_array([r for _, r in comms]), self.max_streams, ctypes.byref(h))
             pl = plan._pipeline = _Pipeline(h)
         return pl
 
@@ -499,8 +502,9 @@ class CommunicationObject:
         start = torch.cuda.Event()
         start.record(stream)
         landed = {}
+        lane_of = {p: k % self.max_streams for k, p in enumerate(peers)}
         for p in peers:
-            sp = self._peer_stream(p, device)
+            sp = self._peer_stream(lane_of[p], device)
             sp.wait_event(start)
             for i in sends_of.get(p, []):
                 _ghx.check(L.ghx_exchange_pack_buffer(plan.h, i, fptrs, nf, sptrs, len(send),
@@ -540,7 +544,7 @@ class CommunicationObject:
         # receive works complete only inside wait(): no polling)
         for w, j, p in rops:
             w.wait()
-            sp = self._peer_stream(p, device)
+            sp = self._peer_stream(lane_of[p], device)
             n = plan.recv[j]["size"]
             with torch.cuda.stream(sp):
                 recv[j][:n].copy_(hr[j][:n], non_blocking=True)
@@ -548,8 +552,8 @@ class CommunicationObject:
                                                     sp.cuda_stream), "unpack_buffer")
         for w in sops:
             w.wait()
-        for p in peers:
-            stream.wait_stream(self._peer_stream(p, device))
+        for lane in set(lane_of.values()):
+            stream.wait_stream(self._peer_stream(lane, device))
 
     # low-level access for benchmarks / tests (no transport)
     def pack_only(self, bis, stream=None):

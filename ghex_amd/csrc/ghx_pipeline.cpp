@@ -4,11 +4,11 @@
 // (include/ghex/device/cuda/stream.hpp:25-73; communication_object.hpp:568-597), posts each send
 // when that buffer's pack has completed (communication_object.hpp:611-637, packer.hpp:73-96) and,
 // with a stream-aware transport such as NCCL, queues each unpack behind its receive on the
-// buffer's stream (:703-714, 751-765). Here each PEER RANK gets a stream: its send buffers are
-// packed there (one launch per buffer), one RCCL group {ncclRecv..., ncclSend...} with that peer
-// follows on the same stream, then its recv buffers are unpacked — so a face message leaves as
-// soon as its own pack is done, while the packs of the other peers' buffers still run, and each
-// unpack starts as soon as its own message has landed. Self messages (periodic wrap onto the same
+// buffer's stream (:703-714, 751-765). Here each PEER RANK rides one of a few streams (lanes):
+// its send buffers are packed there (one launch per buffer), one RCCL group {ncclRecv...,
+// ncclSend...} with that peer follows on the same stream, then its recv buffers are unpacked — so
+// a face message leaves as soon as its own pack is done, while the packs of the other lanes'
+// buffers still run, and each unpack starts as soon as its own message has landed. Self messages (periodic wrap onto the same
 // rank) are packed and unpacked on the caller's stream, never through RCCL. The caller's stream
 // then waits for every peer stream.
 //
@@ -88,22 +88,27 @@ struct pipeline
         int32_t rank = -1;
         ncclComm_t comm = nullptr;
         int32_t comm_peer = 0;     // the peer's rank inside `comm`
-        hipStream_t stream = nullptr;
-        hipEvent_t done = nullptr;
+        int lane = 0;              // which of the pipeline's streams carries this peer
         std::vector<int> sends, recvs;  // buffer indices, in matching order on both sides
     };
     const exchange_plan* ex = nullptr;
     std::vector<peer> peers;                    // issue order (global rounds)
     std::vector<std::pair<int, int>> local;     // (send, recv) buffers of self messages
+    // Peer k rides stream k mod S (S = max_streams): the device runs few hardware queues
+    // (GPU_MAX_HW_QUEUES, 4 by default), and streams beyond them share queues in an order
+    // nobody chooses; dealing the peers over S streams in round order keeps each stream's
+    // sequence in the global round order (so the cross-rank argument above still holds) and
+    // puts the first S peers — the order every rank agrees on — on distinct streams.
+    std::vector<hipStream_t> lanes;
+    std::vector<hipEvent_t> lane_done;
     hipEvent_t start = nullptr;
 
     ~pipeline()
     {
-        for (auto& p : peers)
-        {
-            if (p.done) (void)hipEventDestroy(p.done);
-            if (p.stream) (void)hipStreamDestroy(p.stream);
-        }
+        for (auto e : lane_done)
+            if (e) (void)hipEventDestroy(e);
+        for (auto s : lanes)
+            if (s) (void)hipStreamDestroy(s);
         if (start) (void)hipEventDestroy(start);
     }
 
@@ -113,28 +118,30 @@ struct pipeline
         if (ns < int(ex->send.size()) || nr < int(ex->recv.size()))
             throw invalid("pointer arrays do not cover the exchange's buffers");
         hip_check(hipEventRecord(start, stream), "hipEventRecord");
+        for (hipStream_t l : lanes) hip_check(hipStreamWaitEvent(l, start, 0), "hipStreamWaitEvent");
         for (const auto& p : peers)
         {
-            hip_check(hipStreamWaitEvent(p.stream, start, 0), "hipStreamWaitEvent");
+            hipStream_t ps = lanes[size_t(p.lane)];
             for (int i : p.sends)
-                if (ex->execute_buffer(0, i, fptr, nf, sbuf, ns, p.stream) != GHX_OK)
+                if (ex->execute_buffer(0, i, fptr, nf, sbuf, ns, ps) != GHX_OK)
                     throw hip_error(std::string("pack: ") + get_error());
             const auto& R = rccl();
             nccl_check(R.GroupStart(), "ncclGroupStart");
             for (int j : p.recvs)
                 nccl_check(R.Recv(rbuf[j], size_t(ex->recv[size_t(j)].size), ncclInt8, p.comm_peer,
-                                  p.comm, p.stream),
+                                  p.comm, ps),
                            "ncclRecv");
             for (int i : p.sends)
                 nccl_check(R.Send(sbuf[i], size_t(ex->send[size_t(i)].size), ncclInt8, p.comm_peer,
-                                  p.comm, p.stream),
+                                  p.comm, ps),
                            "ncclSend");
             nccl_check(R.GroupEnd(), "ncclGroupEnd");
             for (int j : p.recvs)
-                if (ex->execute_buffer(1, j, fptr, nf, rbuf, nr, p.stream) != GHX_OK)
+                if (ex->execute_buffer(1, j, fptr, nf, rbuf, nr, ps) != GHX_OK)
                     throw hip_error(std::string("unpack: ") + get_error());
-            hip_check(hipEventRecord(p.done, p.stream), "hipEventRecord");
         }
+        for (size_t l = 0; l < lanes.size(); ++l)
+            hip_check(hipEventRecord(lane_done[l], lanes[l]), "hipEventRecord");
         for (const auto& [i, j] : local)
         {
             if (ex->execute_buffer(0, i, fptr, nf, sbuf, ns, stream) != GHX_OK)
@@ -146,7 +153,7 @@ struct pipeline
             if (ex->execute_buffer(1, j, fptr, nf, rbuf, nr, stream) != GHX_OK)
                 throw hip_error(std::string("unpack: ") + get_error());
         }
-        for (const auto& p : peers) hip_check(hipStreamWaitEvent(stream, p.done, 0), "hipStreamWaitEvent");
+        for (hipEvent_t e : lane_done) hip_check(hipStreamWaitEvent(stream, e, 0), "hipStreamWaitEvent");
     }
 };
 }  // namespace ghx
@@ -229,10 +236,11 @@ int ghx_rccl_comm_check(void* comm)
 
 int ghx_pipeline_create(ghx_exchange* ex, int32_t my_rank, int32_t n_peers,
                         const int32_t* peer_ranks, void* const* comms, const int32_t* comm_ranks,
-                        ghx_pipeline** out)
+                        int32_t max_streams, ghx_pipeline** out)
 {
     return guarded([&] {
         if (!ex || !out) throw invalid("null argument");
+        if (max_streams < 1) throw invalid("max_streams must be >= 1");
         if (n_peers < 0 || (n_peers > 0 && (!peer_ranks || !comms || !comm_ranks)))
             throw invalid("bad peer arrays");
         *out = nullptr;
@@ -270,11 +278,18 @@ int ghx_pipeline_create(ghx_exchange* ex, int32_t my_rank, int32_t n_peers,
                 if (ex->recv[j].rank == p.rank) p.recvs.push_back(int(j)), routed_r[j] = 1;
             std::sort(p.sends.begin(), p.sends.end(), order(ex->send));
             std::sort(p.recvs.begin(), p.recvs.end(), order(ex->recv));
+            p.lane = int(k % max_streams);
             pl->peers.push_back(p);
-            auto& q = pl->peers.back();
-            hip_check(hipStreamCreateWithPriority(&q.stream, hipStreamNonBlocking, greatest),
+        }
+        const int n_lanes = std::min<int>(max_streams, n_peers);
+        pl->lanes.assign(size_t(n_lanes), nullptr);
+        pl->lane_done.assign(size_t(n_lanes), nullptr);
+        for (int l = 0; l < n_lanes; ++l)
+        {
+            hip_check(hipStreamCreateWithPriority(&pl->lanes[size_t(l)], hipStreamNonBlocking, greatest),
                       "hipStreamCreateWithPriority");
-            hip_check(hipEventCreateWithFlags(&q.done, hipEventDisableTiming), "hipEventCreate");
+            hip_check(hipEventCreateWithFlags(&pl->lane_done[size_t(l)], hipEventDisableTiming),
+                      "hipEventCreate");
         }
         // everything else must be a self message: recv j <- the send buffer of the same pair
         for (size_t j = 0; j < ex->recv.size(); ++j)

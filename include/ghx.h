@@ -339,7 +339,10 @@ int ghx_rccl_comm_check(void* comm);
  * each peer, in the given order, on its own greatest-priority stream: pack of its send buffers,
  * one RCCL group {recv..., send...} on comms[k] (the peer is rank comm_ranks[k] there), unpack of
  * its recv buffers. Messages of one pair are issued in (tag, domain pair) order on both sides.
- * Buffers of ranks not listed must be self messages (my_rank): packed and unpacked on the
+ * Peer k rides stream k mod max_streams (the device has few hardware queues, 4 by default:
+ * streams beyond them share queues in an order no one chooses; dealt this way every stream
+ * still runs its peers in the global order). Buffers of ranks not listed must be self messages
+ * (my_rank): packed and unpacked on the
  * caller's stream. ghx_pipeline_run enqueues all of it; the caller's stream then waits for every
  * peer stream (no host synchronisation). Every rank must list its peers in one global order
  * consistent across ranks (e.g. round-robin tournament rounds) so that no wait cycle can form
@@ -347,7 +350,7 @@ int ghx_rccl_comm_check(void* comm);
 typedef struct ghx_pipeline ghx_pipeline;
 int ghx_pipeline_create(ghx_exchange* ex, int32_t my_rank, int32_t n_peers,
                         const int32_t* peer_ranks, void* const* comms, const int32_t* comm_ranks,
-                        ghx_pipeline** out);
+                        int32_t max_streams, ghx_pipeline** out);
 int ghx_pipeline_run(const ghx_pipeline* pl, void* const* field_ptrs, int32_t n_fields,
                      void* const* send_buffers, int32_t n_send, void* const* recv_buffers,
                      int32_t n_recv, ghx_stream stream);
