@@ -13,14 +13,24 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import argparse
     import torch
     from ghex_amd import _ghx
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tune", default="", help="key=value,... (ghx_tune) before planning")
+    ap.add_argument("--pitches", default="516,517,518,520,524,528,532", help="x extents")
+    ap.add_argument("--zs", default="512,256,128,32", help="z planes")
+    args = ap.parse_args()
     L = _ghx.lib()
+    _ghx.call("ghx_tune", b"reset", 0)
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _ghx.call("ghx_tune", k.encode(), int(v))
     H, NY = 2, 512
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream()
-    for ex in (516, 517, 518, 520, 524, 528, 532):
-        for nz in (512, 256, 128, 32):
+    for ex in (int(x) for x in args.pitches.split(",")):
+        for nz in (int(z) for z in args.zs.split(",")):
             ez = nz + 2 * H
             field = torch.zeros((ez, NY + 2 * H, ex), dtype=torch.float64, device=dev)
             d = _ghx.FieldDesc()
@@ -71,7 +81,7 @@ def main():
                 a = row + x0 * 8
                 parts += [a // 128, (a + 8 * H - 1) // 128]
             lines = np.unique(np.concatenate([p.ravel() for p in parts]))
-            print(json.dumps({"x_extent": ex, "pitch": pitch, "z_planes": nz, "us": round(us, 2),
+            print(json.dumps({"tune": args.tune, "x_extent": ex, "pitch": pitch, "z_planes": nz, "us": round(us, 2),
                               "lines": len(lines), "Glines_per_s": round(len(lines) / us / 1e3, 1),
                               "footprint_MB": round(field.numel() * 8 / 1e6, 1)}), flush=True)
             L.ghx_plan_destroy(h)
