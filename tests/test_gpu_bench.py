@@ -1,0 +1,53 @@
+"""bench.py's contract on the GPU box, at a small size: one JSON line with the metric's fields, the
+roofline / cpu-free extras, a verified exchange; and the N>1 path through bench.py's own rank
+spawning (`--gpus 2 --rehearse`: both ranks on the one GPU, gloo + host staging, the pipelined
+exchange included). Each run is a child process bounded by a timeout."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _bench(*args, timeout=150):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                       capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_line_n1_small():
+    d = _bench("--N", "64", "--steps", "12", "--warmup", "3", "--no-cpu-baseline")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["verified"] is True and d["n_gpus"] == 1 and d["steps"] == 12 and d["warmup"] == 3
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["launch_us"] > 0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["algorithmic_bytes_per_launch"] == 2 * (68 ** 3 - 64 ** 3) * 8
+    assert "cold_clean_launch_us" in r and "fused_self" in d
+    assert d["fused_self"]["bytes_moved"] == 3 * (68 ** 3 - 64 ** 3) * 8
+    assert "extras_error" not in d, d.get("extras_error")
+
+
+def test_bench_spawns_two_ranks_rehearsal():
+    d = _bench("--gpus", "2", "--rehearse", "--N", "64", "--steps", "10", "--warmup", "2",
+               "--no-cold", timeout=240)
+    assert d["n_gpus"] == 2 and d["verified"] is True
+    assert d["config"]["decomposition"] == [2, 1, 1] and d["config"]["world_size"] == 2
+    assert d["exchange_pipelined"]["verified"] is True
+    assert "extras_error" not in d, d.get("extras_error")
