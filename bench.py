@@ -395,11 +395,16 @@ def main():
         if rank == 0 and printed.acquire(blocking=False):
             print(json.dumps(o), flush=True)
 
+    extras_done = threading.Event()
+
     def watchdog():
-        if not done.wait(args.extras_timeout):
+        # the extras and the teardown after them are bounded: a rank stuck in a collective (a
+        # peer failed in the extras) prints the line without them and leaves
+        if not extras_done.wait(args.extras_timeout):
             o = dict(out)
             o["extras_error"] = f"extras exceeded {args.extras_timeout:.0f} s; printed without them"
             emit(o)
+        if not done.wait(60.0 if extras_done.is_set() else 5.0):
             sys.stdout.flush()
             os._exit(0)
 
@@ -408,11 +413,13 @@ def main():
         extras(args, torch, dist, dev, stream, out, locals())
     except Exception as e:  # reported, never fatal for the headline measurement
         out["extras_error"] = f"{type(e).__name__}: {str(e)[:300]}"
-    done.set()
+    extras_done.set()
     emit(out)
+    sys.stdout.flush()
     if distributed:
         barrier()
         dist.destroy_process_group()
+    done.set()
 
 
 def extras(args, torch, dist, dev, stream, out, v):
