@@ -309,6 +309,12 @@ struct communication_options
     bool fuse_self = true;                // all-self exchanges as one launch
     bool self_through_transport = false;  // route self messages through the transport too
                                           // (transport testing; oomph also sends to self)
+    // per-peer pipeline (the reference's per-buffer streams + send as packed,
+    // device/cuda/stream.hpp:25-73, communication_object.hpp:568-637, 703-767): each peer's
+    // buffers packed on one of `max_streams` lanes, its group posted there
+    // (transport::exchange_peer), its buffers unpacked there; peers in the global round order
+    bool pipelined = false;
+    int max_streams = 4;
 };
 
 // communication_object<grid, domain_id> (make_communication_object, :1105-1112)
@@ -345,6 +351,9 @@ class communication_object
     options m_opt;
     hipStream_t m_stream = nullptr;
     hipEvent_t m_done = nullptr, m_start = nullptr;
+    std::vector<hipStream_t> m_lanes;     // pipelined: the peer streams
+    std::vector<hipEvent_t> m_lane_done;
+    hipEvent_t m_fork = nullptr;
     bool m_valid = false;
     std::map<std::string, std::unique_ptr<plan>> m_plans;
 
@@ -360,15 +369,33 @@ class communication_object
         check_hip(hipStreamCreateWithPriority(&m_stream, hipStreamNonBlocking, hi), "hipStreamCreate");
         check_hip(hipEventCreateWithFlags(&m_done, hipEventDisableTiming), "hipEventCreate");
         check_hip(hipEventCreateWithFlags(&m_start, hipEventDisableTiming), "hipEventCreate");
+        if (m_opt.pipelined)
+        {
+            if (m_opt.max_streams < 1) throw std::runtime_error("max_streams must be >= 1");
+            check_hip(hipEventCreateWithFlags(&m_fork, hipEventDisableTiming), "hipEventCreate");
+            for (int l = 0; l < m_opt.max_streams; ++l)
+            {
+                hipStream_t st;
+                hipEvent_t ev;
+                check_hip(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi), "hipStreamCreate");
+                check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+                m_lanes.push_back(st);
+                m_lane_done.push_back(ev);
+            }
+        }
     }
     communication_object(const communication_object&) = delete;
     communication_object& operator=(const communication_object&) = delete;
     ~communication_object()
     {
         if (m_stream) (void)hipStreamSynchronize(m_stream);
+        for (auto l : m_lanes) (void)hipStreamSynchronize(l);
         m_plans.clear();
         if (m_done) (void)hipEventDestroy(m_done);
         if (m_start) (void)hipEventDestroy(m_start);
+        if (m_fork) (void)hipEventDestroy(m_fork);
+        for (auto e : m_lane_done) (void)hipEventDestroy(e);
+        for (auto l : m_lanes) (void)hipStreamDestroy(l);
         if (m_stream) (void)hipStreamDestroy(m_stream);
     }
 
@@ -551,9 +578,76 @@ class communication_object
         p->mixed = m_opt.fuse_self && !m_opt.self_through_transport && !p->fused && mixed;
         for (auto& b : p->send) p->sptr.push_back(b.data);
         for (auto& b : p->recv) p->rptr.push_back(b.data);
+        if (m_opt.pipelined)
+        {
+            check_ghx(ghx_exchange_split(p->ex), "ghx_exchange_split");
+            p->fused = false;
+            p->mixed = false;
+        }
         auto& ref = *p;
         m_plans.emplace(std::move(key), std::move(p));
         return ref;
+    }
+
+    // peers in the global round order, dealt over the lanes; self messages on the object's
+    // stream (unless routed through the transport); the object's stream joins every lane
+    void run_pipelined(plan& p, std::vector<void*>& fptrs, std::int32_t nf, std::int32_t ns,
+                       std::int32_t nr)
+    {
+        const int me = m_ctx->rank(), world = m_ctx->size();
+        const bool self_tr = m_opt.self_through_transport;
+        std::vector<int> peers;
+        for (auto* v : {&p.send, &p.recv})
+            for (auto& b : *v)
+                if ((b.rank != me || self_tr) &&
+                    std::find(peers.begin(), peers.end(), b.rank) == peers.end())
+                    peers.push_back(b.rank);
+        std::sort(peers.begin(), peers.end(), [&](int a, int b) {
+            const int ra = round_of(me, a, world), rb = round_of(me, b, world);
+            return ra != rb ? ra < rb : a < b;
+        });
+        check_hip(hipEventRecord(m_fork, m_stream), "hipEventRecord");
+        for (auto l : m_lanes) check_hip(hipStreamWaitEvent(l, m_fork, 0), "hipStreamWaitEvent");
+        for (std::size_t k = 0; k < peers.size(); ++k)
+        {
+            const int q = peers[k];
+            hipStream_t lane = m_lanes[k % m_lanes.size()];
+            std::vector<message> sends, recvs;
+            for (std::size_t i = 0; i < p.send.size(); ++i)
+                if (p.send[i].rank == q)
+                {
+                    check_ghx(ghx_exchange_pack_buffer(p.ex, std::int32_t(i), fptrs.data(), nf,
+                                                       p.sptr.data(), ns, lane),
+                              "ghx_exchange_pack_buffer");
+                    sends.push_back({p.send[i].data, p.send[i].size, q, p.send[i].tag});
+                }
+            for (auto& b : p.recv)
+                if (b.rank == q) recvs.push_back({b.data, b.size, q, b.tag});
+            m_ctx->get_transport().exchange_peer(q, sends, recvs, lane);
+            for (std::size_t j = 0; j < p.recv.size(); ++j)
+                if (p.recv[j].rank == q)
+                    check_ghx(ghx_exchange_unpack_buffer(p.ex, std::int32_t(j), fptrs.data(), nf,
+                                                         p.rptr.data(), nr, lane),
+                              "ghx_exchange_unpack_buffer");
+        }
+        if (!self_tr)
+        {
+            for (std::size_t i = 0; i < p.send.size(); ++i)
+                if (p.send[i].rank == me)
+                    check_ghx(ghx_exchange_pack_buffer(p.ex, std::int32_t(i), fptrs.data(), nf,
+                                                       p.sptr.data(), ns, m_stream),
+                              "ghx_exchange_pack_buffer");
+            for (std::size_t j = 0; j < p.recv.size(); ++j)  // recv aliases the send buffer
+                if (p.recv[j].rank == me)
+                    check_ghx(ghx_exchange_unpack_buffer(p.ex, std::int32_t(j), fptrs.data(), nf,
+                                                         p.rptr.data(), nr, m_stream),
+                              "ghx_exchange_unpack_buffer");
+        }
+        for (std::size_t l = 0; l < m_lanes.size(); ++l)
+        {
+            check_hip(hipEventRecord(m_lane_done[l], m_lanes[l]), "hipEventRecord");
+            check_hip(hipStreamWaitEvent(m_stream, m_lane_done[l], 0), "hipStreamWaitEvent");
+        }
     }
 
     communication_handle start(hipStream_t after, std::vector<ghx_exchange_item> items,
@@ -569,7 +663,9 @@ class communication_object
         }
         const auto nf = std::int32_t(fptrs.size());
         const auto ns = std::int32_t(p.sptr.size()), nr = std::int32_t(p.rptr.size());
-        if (p.fused)
+        if (m_opt.pipelined)
+            run_pipelined(p, fptrs, nf, ns, nr);
+        else if (p.fused)
             check_ghx(ghx_exchange_self(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream), "ghx_exchange_self");
         else
         {

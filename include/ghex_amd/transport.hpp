@@ -26,6 +26,7 @@
 #include <stdexcept>
 #include <string>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 namespace ghex_amd
@@ -59,7 +60,29 @@ class transport
     // ranks are matched by tag; a (peer, tag) pair occurs at most once per direction.
     virtual void exchange(const std::vector<message>& sends, const std::vector<message>& recvs,
                           hipStream_t stream) = 0;
+    // The messages with ONE peer, ordered on `stream` (a pipelined exchange posts one such group
+    // per peer, each on its own stream, as soon as that peer's buffers are packed). A transport
+    // whose groups are independent per peer may specialise it; by default it is one exchange().
+    virtual void exchange_peer(int /*peer*/, const std::vector<message>& sends,
+                               const std::vector<message>& recvs, hipStream_t stream)
+    {
+        exchange(sends, recvs, stream);
+    }
 };
+
+// Round of the pair (a, b) in a round-robin tournament over `world` ranks (circle method):
+// every rank meets every other exactly once, at most once per round. Every rank issues its
+// per-peer groups in this one global order, so with streams that run in issue order (shared
+// hardware queues, a communicator's own serialisation) every wait between ranks points to the
+// same or an earlier round and no cycle can form.
+inline int round_of(int a, int b, int world)
+{
+    const int m = world + (world % 2), q = m - 1;
+    if (a > b) std::swap(a, b);
+    if (q <= 0) return 0;
+    if (b == q) return a;
+    return ((a + b) * (m / 2)) % q;
+}
 
 // ---------------------------------------------------------------------------------------------
 // loopback: ranks = threads of one process on one device

@@ -6,9 +6,11 @@
 //                                        grid, two fields (double, float) in ONE exchange; every
 //                                        cell of every rank vs the wrapped global index; twice
 //                                        (the second exchange reuses the cached plan/buffers)
-//   co_demo rccl N H SELF                one rank, RCCL communicator on device 0; SELF=1 sends the
+//   co_demo pipeloop PX PY PZ N H       the same with options.pipelined: per-peer lanes (pack,
+//                                        transport::exchange_peer, unpack per peer, round order)
+//   co_demo rccl N H SELF [PIPE]         one rank, RCCL communicator on device 0; SELF=1 sends the
 //                                        self messages through ncclSend/ncclRecv (group), SELF=0
-//                                        takes the fused self path
+//                                        takes the fused self path; PIPE=1 the pipelined form
 //   co_demo unstructured FILE LEVELS     ranks as threads, domains from FILE (per line:
 //                                        "id n_gids gids... n_outer lids..."), one domain per rank;
 //                                        value(lid, level) = dom*10000 + gid*100 + level
@@ -112,7 +114,7 @@ long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, i
     return bad;
 }
 
-int loopback(int px, int py, int pz, int N, int H)
+int loopback(int px, int py, int pz, int N, int H, bool pipelined = false)
 {
     const int n = px * py * pz;
     loopback_hub hub(n);
@@ -125,7 +127,9 @@ int loopback(int px, int py, int pz, int N, int H)
         th.emplace_back([&, r] {
             try
             {
-                bad += run_structured_rank(ts[std::size_t(r)], {px, py, pz}, N, H, {});
+                communication_object::options opt;
+                opt.pipelined = pipelined;
+                bad += run_structured_rank(ts[std::size_t(r)], {px, py, pz}, N, H, opt);
             }
             catch (const std::exception& e)
             {
@@ -137,7 +141,7 @@ int loopback(int px, int py, int pz, int N, int H)
     return (bad == 0 && errors == 0) ? 0 : 1;
 }
 
-int rccl(int N, int H, int self)
+int rccl(int N, int H, int self, int pipelined = 0)
 {
     check_hip(hipSetDevice(0), "hipSetDevice");
     ncclComm_t comm;
@@ -148,6 +152,7 @@ int rccl(int N, int H, int self)
         rccl_transport t(comm);
         communication_object::options opt;
         opt.self_through_transport = self != 0;
+        opt.pipelined = pipelined != 0;
         bad = run_structured_rank(t, {1, 1, 1}, N, H, opt);
     }
     check_nccl(ncclCommDestroy(comm), "ncclCommDestroy");
@@ -273,7 +278,12 @@ int main(int argc, char** argv)
         if (mode == "loopback" && argc == 7)
             return loopback(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
                             std::atoi(argv[6]));
+        if (mode == "pipeloop" && argc == 7)
+            return loopback(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                            std::atoi(argv[6]), true);
         if (mode == "rccl" && argc == 5) return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
+        if (mode == "rccl" && argc == 6)
+            return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]));
         if (mode == "unstructured" && argc == 4) return unstructured_case(argv[2], std::atoi(argv[3]));
         if (mode == "bench" && argc == 5) return bench(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
     }

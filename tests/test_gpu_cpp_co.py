@@ -115,3 +115,26 @@ def test_co_loopback_unstructured_known_answer(tmp_path, levels):
     assert rc == 0, (lines, err)
     ranks = [l for l in lines if l.get("mode") == "unstructured"]
     assert len(ranks) == 4 and all(l["bad"] == 0 for l in ranks)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,N,H", [((2, 1, 1), 10, 2), ((2, 2, 2), 8, 3), ((3, 1, 2), 7, 2),
+                                       ((1, 1, 2), 10, 2)])
+def test_co_loopback_pipelined(parts, N, H):
+    """options.pipelined: every rank's peers in the global round order over 4 lanes, each peer
+    packed / exchanged (transport::exchange_peer) / unpacked on its lane; every cell."""
+    rc, lines, err = _run(["pipeloop", *parts, N, H])
+    ranks = [l for l in lines if l.get("mode") == "structured"]
+    assert rc == 0, (lines, err)
+    assert len(ranks) == parts[0] * parts[1] * parts[2]
+    assert all(l["bad"] == 0 for l in ranks)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("self_tr", [0, 1])
+def test_co_rccl_pipelined(self_tr):
+    """The pipelined form over the RCCL transport (one rank; self messages through
+    ncclSend/ncclRecv when self_tr)."""
+    rc, lines, err = _run(["rccl", 12, 2, self_tr, 1])
+    assert rc == 0, (lines, err)
+    assert all(l.get("bad", 1) == 0 for l in lines if l.get("mode") == "structured")
