@@ -494,6 +494,9 @@ def extras(args, torch, dist, dev, stream, out, v):
                                               "one RCCL group on the pair's own communicator") +
                                              " and unpack of each peer's buffers on its stream"}
         del cop
+    # the north star's other halo widths, same decomposition, same two-launch step, verified
+    out["halo_widths"] = {str(h): bench_halo(h, v, torch, dist, dev, stream, args)
+                          for h in (1, 3) if h != Hw}
     if world == 1 or args.bulk:
         # zero-copy bulk exchange (BulkCommunicationObject): puts straight into the
         # receivers' halos, no buffers: 2*n*8 bytes moved per step (not the metric's 4*n*8)
@@ -621,6 +624,67 @@ def kernel_durations(torch, dev, stream, fns, M=10, rounds=15):
             times[i].append(e0.elapsed_time(e1) * 1e-3)
     med = [sorted(t)[len(t) // 2] for t in times]
     return tuple(med[i + 1] - med[i] for i in range(len(fns)))
+
+
+def bench_halo(h, v, torch, dist, dev, stream, args):
+    """The headline's step (pack launch + unpack launch, hipGraphs instantiated beforehand) for
+    halo width h on the same decomposition, after a verified full exchange; one dict."""
+    N, world, rank, R, _ghx, L = v["N"], v["world"], v["rank"], v["R"], v["_ghx"], v["L"]
+    parts = DECOMP[world]
+    G = [parts[d] * N for d in range(3)]
+    c = (rank % parts[0], (rank // parts[0]) % parts[1], rank // (parts[0] * parts[1]))
+    first = tuple(c[d] * N for d in range(3))
+    last = tuple((c[d] + 1) * N - 1 for d in range(3))
+    E = N + 2 * h
+    dd = R.DomainDescriptor(rank, first, last)
+    pc = R.make_pattern(v["ctx"], R.HaloGenerator((0, 0, 0), tuple(g - 1 for g in G), (h,) * 6,
+                                                  (True,) * 3), [dd])
+    base = torch.full((E, E, E), -1.0, dtype=torch.float64, device=dev)
+    ar = [torch.arange(N, device=dev, dtype=torch.float64) + first[d] for d in range(3)]
+    base[h:h + N, h:h + N, h:h + N] = (
+        ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)))
+    fd = R.make_field_descriptor(dd, base.permute(2, 1, 0), (h,) * 3, (E,) * 3)
+    co = R.make_communication_object(v["ctx"], staging="host" if args.rehearse else None)
+    bis = [pc(fd)]
+    co.exchange(bis).wait()
+    w = [((torch.arange(E, device=dev) - h + first[d]) % G[d]).to(torch.float64) for d in range(3)]
+    bad = int((base != w[0].view(1, 1, E) + G[0] * (w[1].view(1, E, 1) + G[1] *
+                                                     w[2].view(E, 1, 1))).sum().item())
+    if world > 1:
+        t = torch.tensor([float(bad)], dtype=torch.float64,
+                         device="cpu" if args.rehearse else dev)
+        dist.all_reduce(t)
+        bad = int(t.item())
+    plan = co.plan(bis)
+    send, recv = co.buffers(plan, dev)
+    fptr = _ghx.ptr_array([fd.data_ptr()])
+    sptr = _ghx.ptr_array([x.data_ptr() for x in send])
+    rptr = _ghx.ptr_array([x.data_ptr() for x in recv])
+
+    def pack(s):
+        _ghx.check(L.ghx_exchange_pack(plan.h, fptr, 1, sptr, len(send), s), "pack")
+
+    def unpack(s):
+        _ghx.check(L.ghx_exchange_unpack(plan.h, fptr, 1, rptr, len(recv), s), "unpack")
+
+    def step():
+        s = torch.cuda.current_stream(dev).cuda_stream
+        pack(s)
+        unpack(s)
+    K = min(v["K"], 100)
+    runner = Runner(torch, dev, stream, step, args.steps_per_graph, eager=args.no_graph)
+    runner.prepare(K)
+    runner.run(K)
+    T = v["timed"](lambda: runner.run(K), 1)
+    t_p, t_u = kernel_durations(torch, dev, stream, [pack, unpack])
+    n = E ** 3 - N ** 3
+    out = {"value": round(world * 4 * n * 8 * K / T / 1e9, 2), "unit": "GB/s",
+           "ms_per_step": round(T / K * 1e3, 5), "steps": K, "pack_us": round(t_p * 1e6, 2),
+           "unpack_us": round(t_u * 1e6, 2), "bytes_per_step_per_gpu": 4 * n * 8,
+           "verified": bad == 0}
+    del runner, co, base, fd, bis, send, recv
+    torch.cuda.empty_cache()
+    return out
 
 
 def chain_duration(torch, dev, stream, fn, M=20, rounds=7):
