@@ -381,6 +381,7 @@ def main():
                             "time per step x the kernel's share of the step (pack_us, "
                             "unpack_us: graphs of M steps vs M steps + one more launch, "
                             "replayed interleaved, median differences)",
+        "launch_us_differential": round(dom_d * 1e6, 2),
         "pack_us": round(t_pack * 1e6, 2), "unpack_us": round(t_unpack * 1e6, 2),
         "step_device_us": round(dev_step * 1e6, 2),
         "step_achieved": round(step_bytes / dev_step / 1e9, 1),
@@ -588,7 +589,7 @@ def host_staged(torch, dev, co, plan, send, recv, pack, unpack, timed, step_byte
             "form": "pack, D2H of the whole buffer, H2D, unpack on one stream"}
 
 
-def kernel_durations(torch, dev, stream, fns, M=10, rounds=15):
+def kernel_durations(torch, dev, stream, fns, M=10, rounds=31):
     """Live per-launch durations of the launches `fns` (one step = fns in order) by differencing
     hipGraphs of M steps, M steps + fns[0], M steps + fns[0] + fns[1], ... replayed in interleaved
     rounds (medians). Removes the events' own cost; each includes its dependent-launch boundary."""
@@ -622,8 +623,13 @@ def kernel_durations(torch, dev, stream, fns, M=10, rounds=15):
             e1.record(stream)
             e1.synchronize()
             times[i].append(e0.elapsed_time(e1) * 1e-3)
-    med = [sorted(t)[len(t) // 2] for t in times]
-    return tuple(med[i + 1] - med[i] for i in range(len(fns)))
+    # per-round differences (the graphs of one round run back to back: slow drifts cancel),
+    # then the median over rounds
+    out = []
+    for i in range(len(fns)):
+        d = sorted(times[i + 1][r] - times[i][r] for r in range(rounds))
+        out.append(d[len(d) // 2])
+    return tuple(out)
 
 
 def bench_halo(h, v, torch, dist, dev, stream, args):
