@@ -293,7 +293,9 @@ def main():
     torch.cuda.synchronize(dev)
 
     def timed(fn, k, events=False, box=None):
-        """Host wall time of k calls (barrier + synchronize on both sides, max over ranks); with
+        """Host wall time of k calls, max over ranks: barrier + synchronize, start the clock,
+        the calls, synchronize, stop the clock, barrier (each rank's clock runs from the common
+        start to its own completion; the closing barrier's own latency is not charged). With
         events=True also the device time of the region from HIP events on the launch stream."""
         if distributed:
             barrier()
@@ -305,12 +307,11 @@ def main():
             fn()
         e1.record(stream)
         torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
         if events and box is not None:
             box["s"] = e0.elapsed_time(e1) * 1e-3
         if distributed:
             barrier()
-        dt = time.perf_counter() - t0
-        if distributed:
             dt = all_reduce_host(dt, dist.ReduceOp.MAX)
         return dt
 
