@@ -806,13 +806,19 @@ def bench_config4(torch, dev, ghex_amd, R):
         if fusedp:
             L.ghx_exchange_self(plan.h, fptr, 5, sptr, len(send), s)
         else:
-            L.ghx_exchange_pack(plan.h, fptr, 5, sptr, len(send), s)
-            L.ghx_exchange_unpack(plan.h, fptr, 5, sptr, len(send), s)
+            two(s)
+
+    def two(s):  # the per-rank form at N>1: pack launch + unpack launch
+        L.ghx_exchange_pack(plan.h, fptr, 5, sptr, len(send), s)
+        L.ghx_exchange_unpack(plan.h, fptr, 5, sptr, len(send), s)
     t = _time_graph(torch, dev, step)
+    t2 = _time_graph(torch, dev, two)
     n = E ** 3 - N ** 3
     nbytes = 4 * n * (3 * 8 + 2 * 4)
-    return {"GBps": round(nbytes / t / 1e9, 1), "us_per_exchange": round(t * 1e6, 2),
-            "bytes_per_exchange": nbytes, "verified": ok, "fused_self": fusedp}
+    return {"GBps": round(nbytes / t2 / 1e9, 1), "us_per_exchange": round(t2 * 1e6, 2),
+            "bytes_per_exchange": nbytes, "verified": ok, "form": "pack launch + unpack launch",
+            "fused_self": {"us_per_exchange": round(t * 1e6, 2),
+                           "bytes_moved": 3 * n * (3 * 8 + 2 * 4)} if fusedp else None}
 
 
 def bench_config5(torch, dev, _ghx, levels):
