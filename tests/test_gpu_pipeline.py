@@ -237,3 +237,41 @@ def test_unstructured_cache_sees_in_place_change():
         torch.cuda.synchronize()
         got = buf.view(torch.float64).cpu().numpy()
         np.testing.assert_array_equal(got, lids.astype(np.float64))
+
+
+@pytest.mark.parametrize("rccl_self", [True, False])
+def test_native_pipeline_unstructured_self_exchange(golden_dir, rccl_self):
+    """The reference Python test's fixture (repeated halo gids, a domain exchanging with itself,
+    test/bindings/python/test_unstructured_domain_descriptor.py) with its 4 domains on ONE rank:
+    every message a self message, routed through a 1-rank RCCL communicator (rccl_self) or
+    packed/unpacked locally, per buffer, by the pipeline; value = owner*1000 + 10*gid + level."""
+    import json
+    import os
+    import torch
+    import ghex_amd
+    from ghex_amd import unstructured as U
+    with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
+        fx = json.load(fh)["python_fixture"]
+    L = fx["levels"]
+    items = sorted(fx["domains"].items())
+    ctx = ghex_amd.make_context()
+    dds = [U.DomainDescriptor(int(k), v["all"], v["outer_lids"]) for k, v in items]
+    pc = U.make_pattern(ctx, U.HaloGenerator(), dds)
+    fields, bis = [], []
+    for (k, v), dd in zip(items, dds):
+        f = np.full((len(v["all"]), L), -1, dtype=np.int64)
+        outer = set(v["outer_lids"])
+        for lid, gid in enumerate(v["all"]):
+            if lid not in outer:
+                f[lid] = [int(k) * 1000 + 10 * gid + l for l in range(L)]
+        t = torch.from_numpy(f).cuda()
+        fields.append(t)
+        bis.append(pc(U.make_field_descriptor(dd, t)))
+    co = U.make_communication_object(ctx, pipelined=True, rccl_self=rccl_self)
+    co.exchange(bis).wait()
+    torch.cuda.synchronize()
+    for (k, v), t in zip(items, fields):
+        got = t.cpu().numpy()
+        for lid, gid in enumerate(v["all"]):
+            for l in range(L):
+                assert got[lid, l] % 1000 == 10 * gid + l, (k, lid, gid, int(got[lid, l]))
