@@ -17,11 +17,76 @@ def make_communication_object(context, **options) -> CommunicationObject:
     return CommunicationObject(context, **options)
 
 
+def _corners(index_set):
+    """(first, last) of a box given as the reference binding's index sets do it
+    (bindings/python/src/ghex/structured/regular.py:31-38, 111-135): any object with `ndim` and
+    corner indexing, set[(0,)*ndim] = first cell, set[(-1,)*ndim] = last cell (e.g. a
+    cartesian_sets.ProductSet, or ghex_amd.structured.ProductSet)."""
+    nd = int(index_set.ndim)
+    return (tuple(int(x) for x in index_set[(0,) * nd]),
+            tuple(int(x) for x in index_set[(-1,) * nd]))
+
+
+class UnitRange:
+    """Integers start <= i < stop (the index-set vocabulary of the reference Python binding,
+    bindings/python/src/ghex/structured/cartesian_sets.py)."""
+
+    def __init__(self, start: int, stop: int):
+        self.start, self.stop = int(start), int(stop)
+        if self.stop < self.start:
+            raise ValueError("UnitRange: stop < start")
+
+    def __len__(self):
+        return self.stop - self.start
+
+    def __getitem__(self, i: int) -> int:
+        n = len(self)
+        if not -n <= i < n:
+            raise IndexError(i)
+        return self.start + (i % n)
+
+    def __mul__(self, other):
+        """rx * ry * rz: the product box (cartesian_sets.py's UnitRange.__mul__)."""
+        return ProductSet(self) * other
+
+
+class ProductSet:
+    """The Cartesian product of UnitRanges: a box of cells, indexable by corner tuples."""
+
+    def __init__(self, *ranges: UnitRange):
+        self.ranges = tuple(ranges)
+
+    @classmethod
+    def from_coords(cls, first: Sequence[int], last: Sequence[int]) -> "ProductSet":
+        return cls(*(UnitRange(f, l + 1) for f, l in zip(first, last)))
+
+    @property
+    def ndim(self) -> int:
+        return len(self.ranges)
+
+    @property
+    def shape(self):
+        return tuple(len(r) for r in self.ranges)
+
+    def __getitem__(self, idx):
+        if len(idx) != self.ndim:
+            raise IndexError(idx)
+        return tuple(r[i] for r, i in zip(self.ranges, idx))
+
+    def __mul__(self, other):
+        more = other.ranges if isinstance(other, ProductSet) else (other,)
+        return ProductSet(*self.ranges, *more)
+
+
 class DomainDescriptor:
     """structured::regular::domain_descriptor (include/ghex/structured/regular/domain_descriptor.hpp):
-    an id and the inclusive global first/last coordinates of the owned box."""
+    an id and the inclusive global first/last coordinates of the owned box — given as
+    (id, first, last), or as the reference binding does, (id, sub_domain_indices) with an index
+    set (bindings/python/src/ghex/structured/regular.py:31-38)."""
 
-    def __init__(self, id_: int, first: Sequence[int], last: Sequence[int]):
+    def __init__(self, id_: int, first, last: Sequence[int] = None):
+        if last is None:
+            first, last = _corners(first)
         self._id = int(id_)
         self._first = tuple(int(x) for x in first)
         self._last = tuple(int(x) for x in last)
@@ -52,8 +117,12 @@ class HaloGenerator:
     bindings/python/src/ghex/structured/regular.py:137-139), or the flat C++ list
     (dim0-, dim0+, dim1-, dim1+, ...)."""
 
-    def __init__(self, global_first: Sequence[int], global_last: Sequence[int], halos,
-                 periodicity: Sequence[bool]):
+    def __init__(self, global_first, global_last, halos, periodicity: Sequence[bool] = None):
+        if periodicity is None:
+            # the reference binding's form: (glob_domain_indices, halos, periodicity)
+            # (bindings/python/src/ghex/structured/regular.py:111-135)
+            global_first, global_last, halos, periodicity = (*_corners(global_first), global_last,
+                                                             halos)
         self.global_first = tuple(int(x) for x in global_first)
         self.global_last = tuple(int(x) for x in global_last)
         D = len(self.global_first)

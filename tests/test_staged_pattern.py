@@ -142,3 +142,29 @@ def test_staged_exchange_fills_corners_like_full_pattern(case):
         for a, b in zip(staged[r], full[r]):
             assert (b.data != -1).all()  # fully periodic: every halo cell received
             np.testing.assert_array_equal(a.data, b.data)
+
+
+def test_reference_binding_index_set_signatures():
+    """The reference binding builds descriptors from index sets
+    (bindings/python/src/ghex/structured/regular.py:31-38, 111-135, and its test
+    test/bindings/python/test_structured_domain_descriptor.py): DomainDescriptor(id, set) and
+    HaloGenerator(glob_set, halos, periodicity) give the same boxes as the coordinate forms."""
+    from ghex_amd.structured.regular import (DomainDescriptor, HaloGenerator, ProductSet,
+                                             UnitRange)
+    sub = ProductSet(UnitRange(3, 9), UnitRange(0, 5), UnitRange(2, 4))
+    assert sub.ndim == 3 and sub.shape == (6, 5, 2)
+    assert sub[(0, 0, 0)] == (3, 0, 2) and sub[(-1, -1, -1)] == (8, 4, 3)
+    prod = UnitRange(3, 9) * UnitRange(0, 5) * UnitRange(2, 4)
+    assert prod.shape == sub.shape and prod[(-1, -1, -1)] == sub[(-1, -1, -1)]
+    dd = DomainDescriptor(7, sub)
+    assert dd.domain_id() == 7 and dd.first() == (3, 0, 2) and dd.last() == (8, 4, 3)
+    glob = ProductSet.from_coords((0, 0, 0), (11, 9, 7))
+    assert glob[(-1, -1, -1)] == (11, 9, 7)
+    a = HaloGenerator(glob, ((1, 0), 2, (0, 3)), (True, False, True))
+    b = HaloGenerator((0, 0, 0), (11, 9, 7), (1, 0, 2, 2, 0, 3), (True, False, True))
+    assert a.halos == b.halos and a.periodic == b.periodic
+    assert a(dd) == b(DomainDescriptor(7, (3, 0, 2), (8, 4, 3))) and len(a(dd)) > 0
+    with pytest.raises(IndexError):
+        UnitRange(0, 2)[2]
+    with pytest.raises(ValueError):
+        UnitRange(3, 2)
