@@ -451,10 +451,20 @@ def extras(args, torch, dist, dev, stream, out, v):
         roof["cold_clean_frac"] = round(launch_bytes / t_dom / 1e9 / HBM_PEAK_GBS, 4)
         roof["cold_clean_pack_us"] = round(t_pc * 1e6, 2)
         roof["cold_clean_unpack_us"] = round(t_uc * 1e6, 2)
-        roof["cold_clean_step_GBps"] = round(step_bytes / (t_pc + t_uc) / 1e9, 1)
-        t_dirty = cold_duration(torch, dev, stream, pack if t_dom == t_pc else unpack,
-                                lambda s: fl.add_(1.0))
+        # the step as an application runs it after a stencil sweep: flush, then pack and unpack
+        # back to back (the unpack's halo lines are the ones the pack has just fetched; flushed
+        # separately, each launch above pays its own misses)
+        t_sc = cold_duration(torch, dev, stream, lambda s: (pack(s), unpack(s)), clean)
+        roof["cold_clean_step_us"] = round(t_sc * 1e6, 2)
+        roof["cold_clean_step_GBps"] = round(step_bytes / t_sc / 1e9, 1)
+        dirty = lambda s: fl.add_(1.0)  # noqa: E731
+        t_dirty = cold_duration(torch, dev, stream, pack if t_dom == t_pc else unpack, dirty)
         roof["cold_dirty_launch_us"] = round(t_dirty * 1e6, 2)
+        t_sd = cold_duration(torch, dev, stream, lambda s: (pack(s), unpack(s)), dirty)
+        roof["cold_dirty_step_us"] = round(t_sd * 1e6, 2)
+        if world == 1 and co.fuse_self and co.all_self(plan):
+            v["cold_fused"] = (cold_duration(torch, dev, stream, fused, clean),
+                               cold_duration(torch, dev, stream, fused, dirty))
         del fl
         torch.cuda.empty_cache()
 
@@ -468,6 +478,9 @@ def extras(args, torch, dist, dev, stream, out, v):
             "GBps_moved": round(moved / t_f / 1e9, 1),
             "frac_moved": round(moved / t_f / 1e9 / HBM_PEAK_GBS, 4),
             "exchange_equivalent_GBps": round(step_bytes / t_f / 1e9, 1),
+            **({"cold_clean_launch_us": round(v["cold_fused"][0] * 1e6, 2),
+                "cold_dirty_launch_us": round(v["cold_fused"][1] * 1e6, 2)}
+               if "cold_fused" in v else {}),
             "note": "pack+unpack of the same cells in one launch; the buffer is written but "
                     "never read back, so bytes_moved = 3*n*8 (the metric's 4*n*8 is the "
                     "two-launch step)"}
