@@ -498,6 +498,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 1) throw invalid("mixed_always must be 0 or 1");
             g_tune.mixed_always = value;
         }
+        else if (k == "short_xcds")
+        {
+            if (value < 0 || value > 7) throw invalid("short_xcds must be in 0..7");
+            g_tune.short_xcds = value;
+        }
         else if (k == "xcd_pair")
         {
             if (value < 0 || value > 1) throw invalid("xcd_pair must be 0 or 1");

@@ -74,6 +74,9 @@ struct tuning
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt
                                        // round-robin over the 8 XCDs) at the same time
+    int short_xcds = 0;                // >0 (1..7): deal the short-row tiles to the first this
+                                       // many XCDs only (block b on XCD b mod 8), the other
+                                       // XCDs' L2s stream the long rows meanwhile
     int mixed_always = 0;              // build the mixed self/peer plans even when the self
                                        // messages hold no short rows (tests, measurements)
 };

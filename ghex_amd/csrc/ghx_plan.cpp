@@ -153,6 +153,31 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
             }
         }
         for (; next < rest.size(); ++next) emit(rest[next].first, rest[next].second);
+        if (g_tune.short_xcds > 0 && g_tune.order == 1)
+        {
+            // short-row tiles only at blocks b with b mod 8 < short_xcds (blocks are dealt
+            // round-robin over the 8 XCDs), long-row tiles in the other slots; the k-th tiles of
+            // both halves of a line-sharing pair keep equal (k mod short_xcds) -> same XCD
+            const uint32_t X = uint32_t(g_tune.short_xcds);
+            std::vector<uint32_t> sh, lo, mix;
+            for (size_t k = 0; k < out.size(); k += 2)
+            {
+                auto& dst = segs[out[k]].row_bytes < g_tune.small_row_bytes ? sh : lo;
+                dst.push_back(out[k]);
+                dst.push_back(out[k + 1]);
+            }
+            size_t a = 0, b = 0;
+            for (uint32_t blk = 0; a < sh.size() || b < lo.size(); ++blk)
+            {
+                const bool want_short = (blk % 8) < X;
+                auto& src = (want_short && a < sh.size()) || b >= lo.size() ? sh : lo;
+                size_t& at = &src == &sh ? a : b;
+                mix.push_back(src[at]);
+                mix.push_back(src[at + 1]);
+                at += 2;
+            }
+            out.swap(mix);
+        }
         if (g_tune.order == 4)
         {
             // long-row units first, the short-row units (16-block groups) after them

@@ -387,7 +387,8 @@ def test_full_size_512_h2_checksum():
                                    {"order": 0, "small_tile_rows": 100, "unroll": 2},
                                    {"order": 2, "tile_bytes": 1024, "unroll": 8, "nt": 3},
                                    {"grid_cap": 7, "nt": 1}, {"short_pol": 3},
-                                   {"short_pol": 1, "small_row_bytes": 4096}])
+                                   {"short_pol": 1, "small_row_bytes": 4096},
+                                   {"short_xcds": 3, "small_tile_rows": 64}])
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_tuning_variants_stay_bit_exact(knobs, Hw):
     """Every launch/planning variant (ghx_tune) must produce the same bytes."""
