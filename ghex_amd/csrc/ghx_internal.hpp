@@ -74,6 +74,9 @@ struct tuning
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt
                                        // round-robin over the 8 XCDs) at the same time
+    int lds = 0;                       // 1: pack 8/16-B rows through LDS (copy_tile_lds:
+                                       // whole 64-B blocks read four lanes each, pieces
+                                       // extracted one row per lane)
     int short_xcds = 0;                // >0 (1..7): deal the short-row tiles to the first this
                                        // many XCDs only (block b on XCD b mod 8), the other
                                        // XCDs' L2s stream the long rows meanwhile

@@ -576,6 +576,62 @@ __device__ __forceinline__ bool try_pair(const seg_s& s, const seg_s* segs, cons
     return true;
 }
 
+// LDS-staged pack of a short-row tile (knob "lds"; the north star's stride -> linear transpose
+// through LDS, kept as a measured alternative): each wave takes 64 rows per trip. Phase 1 reads,
+// for each row, the whole aligned 64-B block that holds it, four lanes per block (16 rows per
+// wave instruction, every access a full 16-B vector at a 16-B boundary) and stages the blocks in
+// the wave's LDS slice; phase 2 gives one row per lane: the lane extracts its R-byte piece from
+// LDS and stores it to the lane-linear buffer. The fabric sees the same line requests as the
+// direct form (the blocks are the rows' own lines); L1/TA traffic is 64/R times the direct form's.
+// Rows of R = 8 or 16 bytes whose field offsets are R-aligned (checked by the caller). Blocks are
+// read whole: an aligned 64-B block never crosses a page, so bytes outside the rows are readable.
+constexpr uint32_t kLdsRows = 64;   // rows per wave per trip
+constexpr uint32_t kLdsPitch = 80;  // staged bytes per row: the block + 16 B (spreads LDS banks)
+
+template<int R>
+__device__ __forceinline__ void copy_tile_lds(const seg_s& s, char* __restrict__ field,
+                                              char* __restrict__ buf, uint32_t start, uint32_t end,
+                                              char* lds)
+{
+    using V = vec_t<16>::type;
+    using VR = typename vec_t<R>::type;
+    const uint32_t lane = threadIdx.x & 63u;
+    char* slice = lds + (threadIdx.x >> 6) * (kLdsRows * kLdsPitch);
+    const uint32_t r1 = end / R;
+    for (uint32_t base = start / R + (threadIdx.x >> 6) * kLdsRows; base < r1;
+         base += (kBlock / 64) * kLdsRows)
+    {
+        V v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            const uint32_t row = base + u * 16 + (lane >> 2);
+            if (row < r1)
+            {
+                const uintptr_t a = reinterpret_cast<uintptr_t>(field + field_offset_s(s, row * R));
+                v[u] = vload<V, false>(reinterpret_cast<const char*>(a & ~uintptr_t(63)) + (lane & 3u) * 16);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (base + u * 16 + (lane >> 2) < r1)
+                *reinterpret_cast<V*>(slice + (u * 16 + (lane >> 2)) * kLdsPitch + (lane & 3u) * 16) = v[u];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t row = base + lane;
+        if (row < r1)
+        {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(field + field_offset_s(s, row * R));
+            const VR x = *reinterpret_cast<const VR*>(slice + lane * kLdsPitch + (a & 63u));
+            vstore<VR, false>(buf + row * R, x);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next trip
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 __device__ __forceinline__ int ptr_wlog2(uint64_t p)
 {
     return __builtin_ctzll(p | 16ull);  // log2 of the largest power of two (<= 16) dividing p
@@ -587,10 +643,16 @@ __device__ __forceinline__ int ptr_wlog2(uint64_t p)
 // holds paired segments (knob "pair"); the pair path more than doubles the kernel's VGPRs
 // (156 vs 73 at U=4), so plans without pairs launch the variant that leaves it out.
 template<bool PACK, int U, int NT, typename Seg, bool RUNS = false, bool PAIR = false,
-         bool ILV = false>
+         bool ILV = false, bool LDS = false>
 __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
 {
     const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
+    char* lds = nullptr;
+    if constexpr (LDS)
+    {
+        __shared__ __attribute__((aligned(16))) char stage[(kBlock / 64) * kLdsRows * kLdsPitch];
+        lds = stage;
+    }
     for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
     {
         const uint32_t si = a.tile_seg[2 * t];
@@ -612,6 +674,19 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         if constexpr (PAIR)
         {
             if (try_pair<PACK, U, NT, ILV>(s, segs, a, field, buf, start, end, w)) continue;
+        }
+        if constexpr (LDS && PACK && std::is_same_v<Seg, seg_s>)
+        {
+            if (s.row_bytes == 16 && w >= 4)
+            {
+                copy_tile_lds<16>(s, field, buf, start, end, lds);
+                continue;
+            }
+            if (s.row_bytes == 8 && w >= 3)
+            {
+                copy_tile_lds<8>(s, field, buf, start, end, lds);
+                continue;
+            }
         }
         switch (w)
         {
@@ -941,6 +1016,8 @@ int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid
         hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (pairs == 2)
         hipLaunchKernelGGL((k_copy<false, 4, 0, seg_s, false, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (!pairs && g_tune.lds && direction == 0)  // LDS-staged short rows (knob "lds")
+        hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, false, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (pairs && direction == 0)
         hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (pairs)

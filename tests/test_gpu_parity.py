@@ -388,7 +388,9 @@ def test_full_size_512_h2_checksum():
                                    {"order": 2, "tile_bytes": 1024, "unroll": 8, "nt": 3},
                                    {"grid_cap": 7, "nt": 1}, {"short_pol": 3},
                                    {"short_pol": 1, "small_row_bytes": 4096},
-                                   {"short_xcds": 3, "small_tile_rows": 64}])
+                                   {"short_xcds": 3, "small_tile_rows": 64},
+                                   {"lds": 1}, {"lds": 1, "small_tile_rows": 100}],
+                         ids=lambda d: "-".join(f"{k}={v}" for k, v in d.items()))
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_tuning_variants_stay_bit_exact(knobs, Hw):
     """Every launch/planning variant (ghx_tune) must produce the same bytes."""
@@ -397,6 +399,7 @@ def test_tuning_variants_stay_bit_exact(knobs, Hw):
         for k, v in knobs.items():
             _ghx.call("ghx_tune", k.encode(), v)
         test_single_domain_periodic_fp64((2, 1, 0), Hw, 11)
+        test_single_domain_periodic_fp64((2, 1, 0), Hw, 16)  # 16-B aligned x-face rows
         test_cube_multi_rank_emulated((2, 2, 2))
     finally:
         _ghx.call("ghx_tune", b"reset", 0)

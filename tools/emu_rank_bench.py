@@ -49,6 +49,9 @@ def main():
     dev = torch.device("cuda", 0)
     base = torch.zeros((E, E, E), dtype=torch.float64, device=dev)
     L = _ghx.lib()
+    for kv in filter(None, os.environ.get("GHX_TUNE", "").split(",")):  # e.g. GHX_TUNE=lds=1
+        k, v = kv.split("=")
+        _ghx.call("ghx_tune", k.encode(), int(v))
     # argv: worlds ("2") or world:decomposition ("2:1,1,2")
     for spec in sys.argv[1:] or ["1", "2", "4", "8"]:
         world = int(spec.split(":")[0])
