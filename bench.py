@@ -351,12 +351,18 @@ def main():
         # chains of one kernel alone (graphs of M packs, of M unpacks)
         t_pack, t_unpack = (chain_duration(torch, dev, stream, pack),
                             chain_duration(torch, dev, stream, unpack))
-    dom_name, dom_d = ("pack", t_pack) if t_pack >= t_unpack else ("unpack", t_unpack)
+    # each kernel's own begin-to-end interval (hipExtLaunchKernel start/stop events, the interval
+    # a rocprofv3 kernel trace reports), eager steps, medians
+    k_pack, k_unpack = launch_durations(torch, dev, stream, _ghx, [pack, unpack])
+    if min(k_pack, k_unpack) <= 0:
+        k_pack, k_unpack = t_pack, t_unpack
+    dom_name, dom_d = ("pack", t_pack) if k_pack >= k_unpack else ("unpack", t_unpack)
+    dom_k = max(k_pack, k_unpack)
     # the dominant launch's share of the timed region's device time (HIP events around the K
-    # steps on the launch stream), split by the live differential durations: conservative (the
-    # step's inter-launch gaps are charged to the launches), and within a few % of the rocprofv3
-    # kernel-trace mean of the same launches (profiles/r02_bench_kernels_by_grid.csv)
-    dom_t = dev_step * dom_d / (t_pack + t_unpack)
+    # steps on the launch stream), split in the ratio of the kernels' own durations: conservative
+    # (the step's inter-launch gaps are charged to the launches), and within a few % of the
+    # rocprofv3 kernel-trace mean of the same launches
+    dom_t = dev_step * dom_k / (k_pack + k_unpack)
     launch_bytes = 2 * n_halo * 8  # read n*s + write n*s, either kernel
     achieved = launch_bytes / dom_t / 1e9
     traffic, traffic_src = None, None
@@ -379,9 +385,11 @@ def main():
         "algorithmic_bytes_per_launch": launch_bytes,
         "launch_us": round(dom_t * 1e6, 2),
         "launch_us_source": "HIP events on the launch stream around the K timed steps: device "
-                            "time per step x the kernel's share of the step (pack_us, "
-                            "unpack_us: graphs of M steps vs M steps + one more launch, "
-                            "replayed interleaved, median differences)",
+                            "time per step x the kernel's share of the step, the share from "
+                            "the kernels' own start/stop events (pack_kernel_us, "
+                            "unpack_kernel_us: hipExtLaunchKernel events, eager steps, medians)",
+        "launch_us_kernel_events": round(dom_k * 1e6, 2),
+        "pack_kernel_us": round(k_pack * 1e6, 2), "unpack_kernel_us": round(k_unpack * 1e6, 2),
         "launch_us_differential": round(dom_d * 1e6, 2),
         "pack_us": round(t_pack * 1e6, 2), "unpack_us": round(t_unpack * 1e6, 2),
         "step_device_us": round(dev_step * 1e6, 2),
@@ -603,6 +611,34 @@ def host_staged(torch, dev, co, plan, send, recv, pack, unpack, timed, step_byte
             "form": "pack, D2H of the whole buffer, H2D, unpack on one stream"}
 
 
+def launch_durations(torch, dev, stream, _ghx, fns, reps=41):
+    """Median begin-to-end duration of each kernel launched by `fns` (one step = fns in order,
+    each ONE kernel launch) over `reps` eager steps on `stream`, from the start/stop events
+    libghx records around each kernel (ghx_launch_timing). (0, ...) if a step launched a
+    different number of kernels."""
+    import ctypes
+    s = stream.cuda_stream
+    for _ in range(3):
+        for f in fns:
+            f(s)
+    torch.cuda.synchronize(dev)
+    n = reps * len(fns)
+    ms = (ctypes.c_float * n)()
+    got = ctypes.c_int32()
+    _ghx.call("ghx_launch_timing", 1)
+    try:
+        for _ in range(reps):
+            for f in fns:
+                f(s)
+        _ghx.call("ghx_launch_timing_read", ms, n, ctypes.byref(got))
+    finally:
+        _ghx.call("ghx_launch_timing", 0)
+    if got.value != n:
+        return (0.0,) * len(fns)
+    per = [sorted(ms[i::len(fns)]) for i in range(len(fns))]
+    return tuple(p[len(p) // 2] * 1e-3 for p in per)
+
+
 def kernel_durations(torch, dev, stream, fns, M=10, rounds=31):
     """Live per-launch durations of the launches `fns` (one step = fns in order) by differencing
     hipGraphs of M steps, M steps + fns[0], M steps + fns[0] + fns[1], ... replayed in interleaved
@@ -697,10 +733,12 @@ def bench_halo(h, v, torch, dist, dev, stream, args):
     runner.run(K)
     T = v["timed"](lambda: runner.run(K), 1)
     t_p, t_u = kernel_durations(torch, dev, stream, [pack, unpack])
+    k_p, k_u = launch_durations(torch, dev, stream, _ghx, [pack, unpack])
     n = E ** 3 - N ** 3
     out = {"value": round(world * 4 * n * 8 * K / T / 1e9, 2), "unit": "GB/s",
            "ms_per_step": round(T / K * 1e3, 5), "steps": K, "pack_us": round(t_p * 1e6, 2),
-           "unpack_us": round(t_u * 1e6, 2), "bytes_per_step_per_gpu": 4 * n * 8,
+           "unpack_us": round(t_u * 1e6, 2), "pack_kernel_us": round(k_p * 1e6, 2),
+           "unpack_kernel_us": round(k_u * 1e6, 2), "bytes_per_step_per_gpu": 4 * n * 8,
            "verified": bad == 0}
     del runner, co, base, fd, bis, send, recv
     torch.cuda.empty_cache()

@@ -52,6 +52,9 @@ class ExchangeItem(ctypes.Structure):
 P = ctypes.POINTER
 _SIGS = {
     "ghx_tune": (c_i32, [ctypes.c_char_p, c_i32]),
+    "ghx_launch_timing": (c_i32, [c_i32]),
+    "ghx_launch_timing_read": (c_i32, [ctypes.POINTER(ctypes.c_float), c_i32,
+                                       ctypes.POINTER(c_i32)]),
     "ghx_last_error": (ctypes.c_char_p, []),
     "ghx_version": (ctypes.c_char_p, []),
     "ghx_plan_create": (c_i32, [P(PackEntry), c_i32, c_i32, P(c_vp)]),

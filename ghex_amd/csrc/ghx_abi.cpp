@@ -564,6 +564,22 @@ int ghx_tune(const char* key, int32_t value)
     });
 }
 
+int ghx_launch_timing(int32_t enable)
+{
+    return guarded([&] {
+        ghx::timing_enable(enable != 0);
+        return GHX_OK;
+    });
+}
+
+int ghx_launch_timing_read(float* ms, int32_t cap, int32_t* n)
+{
+    return guarded([&] {
+        if (cap < 0 || (cap > 0 && !ms)) throw invalid("bad ms / cap");
+        return ghx::timing_read(ms, cap, n);
+    });
+}
+
 int ghx_plan_create(const ghx_pack_entry* entries, int32_t n_entries, int32_t direction,
                     ghx_plan** out)
 {

@@ -189,5 +189,7 @@ int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t gr
 int launch_self(const kargs& a, void* stream, uint32_t grid);
 int launch_put(const kargs& a, void* stream, uint32_t grid);
 uint32_t grid_for_tiles(uint32_t n_tiles);
+void timing_enable(bool on);                            // ghx_launch_timing
+int timing_read(float* ms, int32_t cap, int32_t* n);    // ghx_launch_timing_read
 
 }  // namespace ghx

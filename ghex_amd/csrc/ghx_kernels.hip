@@ -16,15 +16,41 @@
 //
 // Variants (tuning, selected at launch): U = vectors in flight per lane per loop trip,
 // NT = cache policy (0 default, 1 non-temporal stores, 2 non-temporal loads and stores).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "ghx_internal.hpp"
 
 namespace ghx
 {
 tuning g_tune{};
+
+// Per-launch kernel timing (ghx_launch_timing): while enabled on a thread, every launch from that
+// thread goes through hipExtLaunchKernelGGL with a start and a stop event, which the runtime
+// records at the kernel's own begin and end (the interval rocprofv3's kernel trace reports),
+// not around the host call. Eager launches only (not during stream capture).
+thread_local std::vector<std::pair<hipEvent_t, hipEvent_t>>* t_timing = nullptr;
+
+template<typename K, typename... A>
+static void launch(K kernel, uint32_t grid, hipStream_t s, A... args)
+{
+    if (t_timing)
+    {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess)
+        {
+            hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, s, e0, e1, 0, args...);
+            t_timing->emplace_back(e0, e1);
+            return;
+        }
+        if (e0) (void)hipEventDestroy(e0);
+    }
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, s, args...);
+}
 
 namespace
 {
@@ -984,10 +1010,10 @@ void launch_nt(const kargs& a, hipStream_t s, uint32_t grid)
 {
     switch (g_tune.nt)
     {
-        case 1: hipLaunchKernelGGL((k_copy<PACK, U, 1, Seg>), dim3(grid), dim3(kBlock), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_copy<PACK, U, 2, Seg>), dim3(grid), dim3(kBlock), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_copy<PACK, U, 3, Seg>), dim3(grid), dim3(kBlock), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_copy<PACK, U, 0, Seg>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        case 1: launch((k_copy<PACK, U, 1, Seg>), grid, s, a); break;
+        case 2: launch((k_copy<PACK, U, 2, Seg>), grid, s, a); break;
+        case 3: launch((k_copy<PACK, U, 3, Seg>), grid, s, a); break;
+        default: launch((k_copy<PACK, U, 0, Seg>), grid, s, a); break;
     }
 }
 
@@ -999,6 +1025,50 @@ void launch_variant(const kargs& a, hipStream_t s, uint32_t grid)
     else launch_nt<Seg, PACK, 4>(a, s, grid);
 }
 }  // namespace
+
+void timing_enable(bool on)
+{
+    if (on && !t_timing) t_timing = new std::vector<std::pair<hipEvent_t, hipEvent_t>>();
+    if (!on && t_timing)
+    {
+        for (auto& e : *t_timing)
+        {
+            (void)hipEventSynchronize(e.second);
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        delete t_timing;
+        t_timing = nullptr;
+    }
+}
+
+int timing_read(float* ms, int32_t cap, int32_t* n)
+{
+    int32_t k = 0;
+    hipError_t bad = hipSuccess;
+    if (t_timing)
+    {
+        for (auto& e : *t_timing)
+        {
+            float t = 0.f;
+            hipError_t r = hipEventSynchronize(e.second);
+            if (r == hipSuccess) r = hipEventElapsedTime(&t, e.first, e.second);
+            if (r != hipSuccess && bad == hipSuccess) bad = r;
+            if (ms && k < cap) ms[k] = t;
+            ++k;
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        t_timing->clear();
+    }
+    if (n) *n = k;
+    if (bad != hipSuccess)
+    {
+        set_error(std::string("launch timing: ") + hipGetErrorString(bad));
+        return GHX_ERR_HIP;
+    }
+    return GHX_OK;
+}
 
 uint32_t grid_for_tiles(uint32_t n_tiles)
 {
@@ -1013,15 +1083,15 @@ int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid
     // plans with paired segments (knob "pair"): one variant, U = 4, default cache policy;
     // pairs == 2: the two rows of a line on alternate lanes of one instruction
     if (pairs == 2 && direction == 0)
-        hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
+        launch((k_copy<true, 4, 0, seg_s, false, true, true>), grid, s, a);
     else if (pairs == 2)
-        hipLaunchKernelGGL((k_copy<false, 4, 0, seg_s, false, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
+        launch((k_copy<false, 4, 0, seg_s, false, true, true>), grid, s, a);
     else if (!pairs && g_tune.lds && direction == 0)  // LDS-staged short rows (knob "lds")
-        hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, false, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
+        launch((k_copy<true, 4, 0, seg_s, false, false, false, true>), grid, s, a);
     else if (pairs && direction == 0)
-        hipLaunchKernelGGL((k_copy<true, 4, 0, seg_s, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
+        launch((k_copy<true, 4, 0, seg_s, false, true>), grid, s, a);
     else if (pairs)
-        hipLaunchKernelGGL((k_copy<false, 4, 0, seg_s, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
+        launch((k_copy<false, 4, 0, seg_s, false, true>), grid, s, a);
     else if (direction == 0) launch_variant<seg_s, true>(a, s, grid);
     else launch_variant<seg_s, false>(a, s, grid);
     const hipError_t e = hipGetLastError();
@@ -1038,10 +1108,10 @@ int launch_self(const kargs& a, void* stream, uint32_t grid)
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (a.pipe)  // software-pipelined tiles (a developer knob): one variant, U = 4
-        hipLaunchKernelGGL((k_self<4, 0, true>), dim3(grid), dim3(kBlock), 0, s, a);
-    else if (g_tune.unroll == 8) hipLaunchKernelGGL((k_self<8, 0>), dim3(grid), dim3(kBlock), 0, s, a);
-    else if (g_tune.unroll == 2) hipLaunchKernelGGL((k_self<2, 0>), dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_self<4, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+        launch((k_self<4, 0, true>), grid, s, a);
+    else if (g_tune.unroll == 8) launch((k_self<8, 0>), grid, s, a);
+    else if (g_tune.unroll == 2) launch((k_self<2, 0>), grid, s, a);
+    else launch((k_self<4, 0>), grid, s, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
     {
@@ -1055,9 +1125,9 @@ int launch_put(const kargs& a, void* stream, uint32_t grid)
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (g_tune.unroll == 8) hipLaunchKernelGGL((k_put<8>), dim3(grid), dim3(kBlock), 0, s, a);
-    else if (g_tune.unroll == 2) hipLaunchKernelGGL((k_put<2>), dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_put<4>), dim3(grid), dim3(kBlock), 0, s, a);
+    if (g_tune.unroll == 8) launch((k_put<8>), grid, s, a);
+    else if (g_tune.unroll == 2) launch((k_put<2>), grid, s, a);
+    else launch((k_put<4>), grid, s, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
     {
@@ -1072,9 +1142,9 @@ int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t gr
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (runs && direction == 0)
-        hipLaunchKernelGGL((k_copy<true, 4, 0, seg_u, true>), dim3(grid), dim3(kBlock), 0, s, a);
+        launch((k_copy<true, 4, 0, seg_u, true>), grid, s, a);
     else if (runs)
-        hipLaunchKernelGGL((k_copy<false, 4, 0, seg_u, true>), dim3(grid), dim3(kBlock), 0, s, a);
+        launch((k_copy<false, 4, 0, seg_u, true>), grid, s, a);
     else if (direction == 0) launch_variant<seg_u, true>(a, s, grid);
     else launch_variant<seg_u, false>(a, s, grid);
     const hipError_t e = hipGetLastError();

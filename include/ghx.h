@@ -64,6 +64,16 @@ typedef void* ghx_stream;
  * include/ghex/structured/pack_kernels.hpp:211-214). */
 int ghx_tune(const char* key, int32_t value);
 
+/* Per-launch kernel durations (measurement; no reference counterpart). ghx_launch_timing(1) makes
+ * every kernel launch issued afterwards BY THIS THREAD record a start and a stop event at the
+ * kernel's own begin and end (hipExtLaunchKernel: the interval a rocprofv3 kernel trace reports);
+ * eager launches only — never enable it around a stream capture. ghx_launch_timing_read waits for
+ * the recorded launches, writes up to `cap` durations in milliseconds (launch order) to `ms`, the
+ * number recorded to `*n`, and releases them; ghx_launch_timing(0) stops recording (and drops
+ * unread records). */
+int ghx_launch_timing(int32_t enable);
+int ghx_launch_timing_read(float* ms, int32_t cap, int32_t* n);
+
 /* Last error message of the calling thread ("" if none). */
 const char* ghx_last_error(void);
 /* Library version string and the offload target it was compiled for ("gfx950"). */

@@ -51,3 +51,39 @@ def test_bench_spawns_two_ranks_rehearsal():
     assert d["config"]["decomposition"] == [2, 1, 1] and d["config"]["world_size"] == 2
     assert d["exchange_pipelined"]["verified"] is True
     assert "extras_error" not in d, d.get("extras_error")
+
+
+def test_launch_timing_records_each_kernel():
+    """ghx_launch_timing: one start/stop pair per kernel launch of this thread, durations > 0,
+    nothing recorded once disabled."""
+    import ctypes
+    import torch
+    from ghex_amd import _ghx
+    L = _ghx.lib()
+    t = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    b = torch.empty(1 << 16, dtype=torch.uint8, device="cuda")
+    d = _ghx.FieldDesc()
+    d.dim, d.elem_size, d.num_components = 1, 1, 1
+    d.layout[0], d.offsets[0], d.extents[0], d.byte_strides[0] = 0, 0, t.numel(), 1
+    box = _ghx.Box()
+    box.first[0], box.last[0] = 4096, 4096 + b.numel() - 1
+    s = torch.cuda.current_stream().cuda_stream
+    ms = (ctypes.c_float * 8)()
+    n = ctypes.c_int32()
+    _ghx.call("ghx_launch_timing", 1)
+    try:
+        for _ in range(3):
+            _ghx.call("ghx_structured_pack", ctypes.byref(d), t.data_ptr(), b.data_ptr(),
+                      ctypes.byref(box), 1, s)
+        _ghx.call("ghx_launch_timing_read", ms, 8, ctypes.byref(n))
+        assert n.value == 3 and all(0 < ms[i] < 100 for i in range(3))
+        _ghx.call("ghx_launch_timing_read", ms, 8, ctypes.byref(n))
+        assert n.value == 0
+    finally:
+        _ghx.call("ghx_launch_timing", 0)
+    _ghx.call("ghx_structured_pack", ctypes.byref(d), t.data_ptr(), b.data_ptr(),
+              ctypes.byref(box), 1, s)
+    _ghx.call("ghx_launch_timing_read", ms, 8, ctypes.byref(n))
+    assert n.value == 0
+    torch.cuda.synchronize()
+    assert torch.equal(b, t[4096:4096 + b.numel()])
