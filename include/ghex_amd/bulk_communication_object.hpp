@@ -1,0 +1,377 @@
+// ghex_amd/bulk_communication_object.hpp — the reference's zero-copy exchange for node-local
+// GPUs in C++ over the C ABI: bulk_communication_object (include/ghex/bulk_communication_object.hpp
+// :206-704), its structured put (include/ghex/structured/rma_put.hpp:204-245) and the CUDA IPC
+// handles (include/ghex/rma/cuda/handle.hpp:20-96), in the same shape as ghex_amd.
+// BulkCommunicationObject (ghex_amd/bulk_communication_object.py):
+//
+//   bulk_communication_object bco(ctx);
+//   bco.add_field(pattern(field_a)); bco.add_field(pattern(field_b));   // same order on every rank
+//   bco.init();                                                         // collective
+//   bco.exchange().wait();                                              // collective
+//
+// Instead of pack -> transport -> unpack, every rank copies its send regions straight into the
+// receiving rank's halo cells: libghx put plans (ghx_put_*: the sender's send halo and the
+// receiver's recv halo of one key describe the same virtual message bytes; one launch per group
+// of up to 64 messages) on the object's stream. Peer fields are mapped once in init(): through
+// IPC handles (ghx_ipc_export/import) for ranks in other processes of this host, directly for
+// ranks that are threads of this process (loopback transport). Ranks on other hosts: throws
+// (their exchanges use communication_object).
+//
+// Epochs (the reference's access guards, include/ghex/rma/access_guard.hpp): exchange() first
+// drains the caller's stream (or the device) so this rank's kernels no longer touch its halos,
+// then a barrier (every target open); it launches the puts, drains them, and passes a second
+// barrier (every halo of every rank written). Barriers are transport all_gathers of nothing.
+// Structured fields only (the reference's bulk object serves structured fields through
+// rma_range_generator; unstructured exchanges use communication_object).
+#pragma once
+
+#include <ghx.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "communication_object.hpp"
+
+namespace ghex_amd
+{
+class bulk_handle
+{
+  public:
+    void wait() {}
+    bool is_ready() { return true; }
+    void progress() {}
+};
+
+class bulk_communication_object
+{
+    struct local_field
+    {
+        const pattern_container* pattern;
+        int local_index;
+        ghx_field_desc desc;
+        void* data;
+        int domain;
+        int j;  // the j-th field registered for this domain on this rank
+    };
+    struct remote_space_key
+    {
+        int remote_id, tag;
+        std::vector<ghx_box> boxes;
+    };
+    struct remote_field
+    {
+        int domain, j;
+        ghx_field_desc desc;
+        unsigned char ipc[64];
+        std::uint64_t offset, raw;
+        std::vector<remote_space_key> recv;
+    };
+    struct remote_rank
+    {
+        std::string host;
+        long pid;
+        std::vector<remote_field> fields;
+    };
+    struct put
+    {
+        ghx_put* h = nullptr;
+        std::vector<void*> dst;
+    };
+
+    context* m_ctx;
+    hipStream_t m_stream = nullptr;
+    std::vector<local_field> m_fields;
+    std::vector<void*> m_src;
+    std::vector<put> m_puts;
+    std::vector<void*> m_imports;
+    bool m_init = false;
+
+    static std::string hostname()
+    {
+        char buf[256] = {0};
+        if (gethostname(buf, sizeof(buf) - 1) != 0) return "?";
+        return buf;
+    }
+    void barrier() { (void)m_ctx->get_transport().all_gather({}); }
+
+    // halos of a local domain: [(remote id, remote rank, tag, local boxes)]
+    static std::vector<std::tuple<int, int, int, std::vector<ghx_box>>> halos(const pattern_container& pc,
+                                                                             int li, int dir)
+    {
+        std::int32_t n = 0;
+        check_ghx(ghx_pattern_num_keys(pc.handle(), li, dir, &n), "ghx_pattern_num_keys");
+        std::vector<std::tuple<int, int, int, std::vector<ghx_box>>> out;
+        for (std::int32_t k = 0; k < n; ++k)
+        {
+            std::int32_t rid = 0, rr = 0, tag = 0, ns = 0;
+            std::int64_t ne = 0;
+            check_ghx(ghx_pattern_key(pc.handle(), li, dir, k, &rid, &rr, &tag, &ns, &ne), "ghx_pattern_key");
+            std::vector<ghx_box> loc(std::size_t(std::max(1, ns))), glo(loc.size());
+            check_ghx(ghx_pattern_key_boxes(pc.handle(), li, dir, k, loc.data(), glo.data(), ns),
+                      "ghx_pattern_key_boxes");
+            loc.resize(std::size_t(ns));
+            out.emplace_back(rid, rr, tag, std::move(loc));
+        }
+        return out;
+    }
+
+    std::vector<char> serialize_mine() const
+    {
+        std::vector<char> out;
+        const std::string host = hostname();
+        detail::put(out, std::int32_t(host.size()));
+        out.insert(out.end(), host.begin(), host.end());
+        detail::put(out, std::int64_t(getpid()));
+        detail::put(out, std::int32_t(m_fields.size()));
+        for (const auto& f : m_fields)
+        {
+            detail::put(out, std::int32_t(f.domain));
+            detail::put(out, std::int32_t(f.j));
+            detail::put(out, f.desc);
+            unsigned char h[64];
+            std::uint64_t off = 0;
+            check_ghx(ghx_ipc_export(f.data, h, &off), "ghx_ipc_export");
+            out.insert(out.end(), reinterpret_cast<char*>(h), reinterpret_cast<char*>(h) + 64);
+            detail::put(out, off);
+            detail::put(out, std::uint64_t(reinterpret_cast<std::uintptr_t>(f.data)));
+            const auto recv = halos(*f.pattern, f.local_index, 1);
+            detail::put(out, std::int32_t(recv.size()));
+            for (const auto& [rid, rr, tag, boxes] : recv)
+            {
+                (void)rr;
+                detail::put(out, std::int32_t(rid));
+                detail::put(out, std::int32_t(tag));
+                detail::put(out, std::int32_t(boxes.size()));
+                for (const auto& b : boxes) detail::put(out, b);
+            }
+        }
+        return out;
+    }
+
+    static remote_rank deserialize(const std::vector<char>& in)
+    {
+        remote_rank r;
+        std::size_t pos = 0;
+        const auto hl = detail::get<std::int32_t>(in, pos);
+        if (hl < 0 || pos + std::size_t(hl) > in.size()) throw std::runtime_error("malformed bulk payload");
+        r.host.assign(in.data() + pos, std::size_t(hl));
+        pos += std::size_t(hl);
+        r.pid = long(detail::get<std::int64_t>(in, pos));
+        const auto nf = detail::get<std::int32_t>(in, pos);
+        for (std::int32_t i = 0; i < nf; ++i)
+        {
+            remote_field f;
+            f.domain = detail::get<std::int32_t>(in, pos);
+            f.j = detail::get<std::int32_t>(in, pos);
+            f.desc = detail::get<ghx_field_desc>(in, pos);
+            if (pos + 64 > in.size()) throw std::runtime_error("malformed bulk payload");
+            std::memcpy(f.ipc, in.data() + pos, 64);
+            pos += 64;
+            f.offset = detail::get<std::uint64_t>(in, pos);
+            f.raw = detail::get<std::uint64_t>(in, pos);
+            const auto nk = detail::get<std::int32_t>(in, pos);
+            for (std::int32_t k = 0; k < nk; ++k)
+            {
+                remote_space_key key;
+                key.remote_id = detail::get<std::int32_t>(in, pos);
+                key.tag = detail::get<std::int32_t>(in, pos);
+                const auto nb = detail::get<std::int32_t>(in, pos);
+                for (std::int32_t b = 0; b < nb; ++b) key.boxes.push_back(detail::get<ghx_box>(in, pos));
+                f.recv.push_back(std::move(key));
+            }
+            r.fields.push_back(std::move(f));
+        }
+        return r;
+    }
+
+    struct msg
+    {
+        int src;                     // index into m_fields
+        std::vector<ghx_box> sboxes;  // sender's local coordinates
+        std::pair<int, int> target;  // (rank, index in that rank's field list)
+        const std::vector<ghx_box>* tboxes;
+    };
+
+    void make_put(const std::vector<msg>& chunk, const std::vector<std::pair<int, int>>& dsts,
+                  const std::vector<remote_rank>& all, const std::map<std::pair<int, int>, void*>& ptr_of)
+    {
+        const auto n = chunk.size();
+        std::vector<ghx_pack_entry> src(n), dst(n);
+        for (std::size_t b = 0; b < n; ++b)
+        {
+            const auto& m = chunk[b];
+            std::memset(&src[b], 0, sizeof(ghx_pack_entry));
+            std::memset(&dst[b], 0, sizeof(ghx_pack_entry));
+            src[b].field = m_fields[std::size_t(m.src)].desc;
+            src[b].field_slot = m.src;
+            src[b].buffer_slot = std::int32_t(b);
+            src[b].boxes = m.sboxes.data();
+            src[b].n_boxes = std::int32_t(m.sboxes.size());
+            dst[b].field = all[std::size_t(m.target.first)].fields[std::size_t(m.target.second)].desc;
+            dst[b].field_slot =
+                std::int32_t(std::find(dsts.begin(), dsts.end(), m.target) - dsts.begin());
+            dst[b].buffer_slot = std::int32_t(b);
+            dst[b].boxes = m.tboxes->data();
+            dst[b].n_boxes = std::int32_t(m.tboxes->size());
+        }
+        put p;
+        check_ghx(ghx_put_create(src.data(), std::int32_t(n), dst.data(), std::int32_t(n), &p.h), "ghx_put_create");
+        for (const auto& t : dsts) p.dst.push_back(ptr_of.at(t));
+        m_puts.push_back(std::move(p));
+    }
+
+  public:
+    explicit bulk_communication_object(context& ctx)
+    : m_ctx{&ctx}
+    {
+        int lo = 0, hi = 0;
+        check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+        check_hip(hipStreamCreateWithPriority(&m_stream, hipStreamNonBlocking, hi), "hipStreamCreate");
+    }
+    bulk_communication_object(const bulk_communication_object&) = delete;
+    bulk_communication_object& operator=(const bulk_communication_object&) = delete;
+    ~bulk_communication_object()
+    {
+        if (m_stream) (void)hipStreamSynchronize(m_stream);
+        for (auto& p : m_puts) ghx_put_destroy(p.h);
+        for (auto b : m_imports) ghx_ipc_close(b);
+        if (m_stream) (void)hipStreamDestroy(m_stream);
+    }
+
+    hipStream_t stream() const { return m_stream; }
+    bool initialized() const { return m_init; }
+
+    // add_field(pattern(field)) (bulk_communication_object.hpp:430-470)
+    template<typename Field>
+    void add_field(buffer_info<Field> bi)
+    {
+        static_assert(std::is_same_v<std::decay_t<decltype(bi.field->desc())>, ghx_field_desc>,
+                      "bulk (zero-copy) exchange is implemented for structured fields");
+        if (m_init) throw std::runtime_error("this bulk communication object has been initialized already");
+        if (m_fields.size() == GHX_MAX_SLOTS) throw std::runtime_error("at most 64 fields per bulk object");
+        local_field f{bi.pattern, bi.local_index, bi.field->desc(),
+                      const_cast<void*>(static_cast<const void*>(bi.field->data())), int(bi.field->domain_id()), 0};
+        for (const auto& g : m_fields) f.j += g.domain == f.domain;
+        m_fields.push_back(f);
+    }
+
+    // init() (bulk_communication_object.hpp:472-560): collective
+    void init()
+    {
+        if (m_init) return;
+        const int me = m_ctx->rank();
+        const auto gathered = m_ctx->get_transport().all_gather(serialize_mine());
+        std::vector<remote_rank> all;
+        for (const auto& g : gathered) all.push_back(deserialize(g));
+        const auto& mine = all[std::size_t(me)];
+        for (std::size_t r = 0; r < all.size(); ++r)
+            if (all[r].host != mine.host)
+                throw std::runtime_error("rank " + std::to_string(r) + " is on another host (" + all[r].host +
+                                         "): zero-copy puts need node-local peers; use communication_object");
+        std::map<std::tuple<int, int, int>, std::pair<int, int>> target;  // (rank, domain, j)
+        for (std::size_t r = 0; r < all.size(); ++r)
+            for (std::size_t i = 0; i < all[r].fields.size(); ++i)
+                target[{int(r), all[r].fields[i].domain, all[r].fields[i].j}] = {int(r), int(i)};
+        std::vector<msg> msgs;
+        for (std::size_t k = 0; k < m_fields.size(); ++k)
+        {
+            const auto& f = m_fields[k];
+            for (auto& [rid, rr, tag, boxes] : halos(*f.pattern, f.local_index, 0))
+            {
+                const auto t = target.find({rr, rid, f.j});
+                if (t == target.end())
+                    throw std::runtime_error("rank " + std::to_string(rr) + " registered no field #" +
+                                             std::to_string(f.j) + " for domain " + std::to_string(rid));
+                const auto& tf = all[std::size_t(t->second.first)].fields[std::size_t(t->second.second)];
+                const std::vector<ghx_box>* tb = nullptr;
+                for (const auto& key : tf.recv)
+                    if (key.remote_id == f.domain && key.tag == tag) tb = &key.boxes;
+                if (!tb)
+                    throw std::runtime_error("no receive halo on rank " + std::to_string(rr) + " for domain " +
+                                             std::to_string(f.domain) + ", tag " + std::to_string(tag));
+                msgs.push_back({int(k), std::move(boxes), t->second, tb});
+            }
+        }
+        // map every target field once: own fields and fields of ranks in this process directly,
+        // the others through their IPC handles
+        std::map<std::pair<int, int>, void*> ptr_of;
+        for (const auto& m : msgs)
+        {
+            if (ptr_of.count(m.target)) continue;
+            const auto& owner = all[std::size_t(m.target.first)];
+            const auto& tf = owner.fields[std::size_t(m.target.second)];
+            if (owner.pid == mine.pid)
+                ptr_of[m.target] = reinterpret_cast<void*>(std::uintptr_t(tf.raw));
+            else
+            {
+                void *base = nullptr, *ptr = nullptr;
+                check_ghx(ghx_ipc_import(tf.ipc, tf.offset, &base, &ptr), "ghx_ipc_import");
+                m_imports.push_back(base);
+                ptr_of[m.target] = ptr;
+            }
+        }
+        // put plans of <= 64 messages and <= 64 target fields
+        std::vector<msg> chunk;
+        std::vector<std::pair<int, int>> dsts;
+        for (std::size_t i = 0; i <= msgs.size(); ++i)
+        {
+            const bool end = i == msgs.size();
+            const bool full = !end && (chunk.size() == GHX_MAX_SLOTS ||
+                                       (std::find(dsts.begin(), dsts.end(), msgs[i].target) == dsts.end() &&
+                                        dsts.size() == GHX_MAX_SLOTS));
+            if ((end || full) && !chunk.empty())
+            {
+                make_put(chunk, dsts, all, ptr_of);
+                chunk.clear();
+                dsts.clear();
+            }
+            if (end) break;
+            if (std::find(dsts.begin(), dsts.end(), msgs[i].target) == dsts.end()) dsts.push_back(msgs[i].target);
+            chunk.push_back(std::move(msgs[i]));
+        }
+        for (const auto& f : m_fields) m_src.push_back(f.data);
+        m_init = true;
+    }
+
+    // exchange() (bulk_communication_object.hpp:600-704): collective. `after`: the stream this
+    // rank's kernels that read or write the fields run on (null: the whole device is drained).
+    bulk_handle exchange(hipStream_t after = nullptr)
+    {
+        if (!m_init) init();
+        if (after) check_hip(hipStreamSynchronize(after), "hipStreamSynchronize");
+        else check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        barrier();  // every target open
+        for (auto& p : m_puts)
+            check_ghx(ghx_put_execute(p.h, m_src.data(), std::int32_t(m_src.size()), p.dst.data(),
+                                      std::int32_t(p.dst.size()), m_stream),
+                      "ghx_put_execute");
+        check_hip(hipStreamSynchronize(m_stream), "hipStreamSynchronize");
+        barrier();  // every halo of every rank written
+        return {};
+    }
+
+    // bytes moved per exchange by this rank's puts
+    std::uint64_t bytes_per_exchange() const
+    {
+        std::uint64_t tot = 0;
+        for (const auto& p : m_puts)
+        {
+            std::uint64_t b = 0;
+            check_ghx(ghx_put_info(p.h, &b, nullptr), "ghx_put_info");
+            tot += b;
+        }
+        return tot;
+    }
+    std::size_t num_puts() const { return m_puts.size(); }
+};
+
+inline bulk_communication_object make_bulk_communication_object(context& ctx)
+{
+    return bulk_communication_object(ctx);
+}
+}  // namespace ghex_amd

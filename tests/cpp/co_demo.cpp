@@ -8,6 +8,9 @@
 //                                        (the second exchange reuses the cached plan/buffers)
 //   co_demo pipeloop PX PY PZ N H       the same with options.pipelined: per-peer lanes (pack,
 //                                        transport::exchange_peer, unpack per peer, round order)
+//   co_demo bulkloop PX PY PZ N H       the same two fields through the C++
+//                                        bulk_communication_object (zero-copy puts between the
+//                                        thread-ranks' fields, no buffers)
 //   co_demo rccl N H SELF [PIPE]         one rank, RCCL communicator on device 0; SELF=1 sends the
 //                                        self messages through ncclSend/ncclRecv (group), SELF=0
 //                                        takes the fused self path; PIPE=1 the pipelined form
@@ -19,6 +22,7 @@
 //   co_demo bench N H ITERS              one rank, host-inclusive microseconds per exchange
 //                                        (exchange + wait) on the fused self path
 // Prints one JSON line per rank / result; exit status 0 iff every cell matched.
+#include <ghex_amd/bulk_communication_object.hpp>
 #include <ghex_amd/communication_object.hpp>
 #include <ghex_amd/data_descriptor.hpp>
 #include <ghex_amd/field_descriptor.hpp>
@@ -58,7 +62,7 @@ struct cube
 
 // one rank: its domain, two fields, exchange twice, count bad cells
 long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, int H,
-                         communication_object::options opt, int reps = 2)
+                         communication_object::options opt, int reps = 2, bool bulk = false)
 {
     check_hip(hipSetDevice(0), "hipSetDevice");
     context ctx(t);
@@ -88,13 +92,22 @@ long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, i
     structured::field_descriptor<double, 3> fd(r, dd, {H, H, H}, {cb.E, cb.E, cb.E}, {2, 1, 0});
     structured::field_descriptor<float, 3> ff(r, df, {H, H, H}, {cb.E, cb.E, cb.E}, {2, 1, 0});
     communication_object co(ctx, opt);
+    bulk_communication_object bco(ctx);
+    if (bulk)
+    {
+        bco.add_field(pattern(fd));
+        bco.add_field(pattern(ff));
+        bco.init();
+    }
     long bad = 0;
     for (int rep = 0; rep < reps; ++rep)
     {
         check_hip(hipMemcpy(dd, hd.data(), std::size_t(E3) * 8, hipMemcpyHostToDevice), "hipMemcpy");
         check_hip(hipMemcpy(df, hf.data(), std::size_t(E3) * 4, hipMemcpyHostToDevice), "hipMemcpy");
-        auto h = co.exchange(pattern(fd), pattern(ff));
-        h.wait();
+        if (bulk)
+            bco.exchange().wait();
+        else
+            co.exchange(pattern(fd), pattern(ff)).wait();
         std::vector<double> od(static_cast<std::size_t>(E3));
         std::vector<float> of(static_cast<std::size_t>(E3));
         check_hip(hipMemcpy(od.data(), dd, std::size_t(E3) * 8, hipMemcpyDeviceToHost), "hipMemcpy");
@@ -108,13 +121,14 @@ long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, i
                     bad += of[std::size_t(cb.idx(x, y, z))] != float(e + 1.0);
                 }
     }
-    std::printf("{\"mode\":\"structured\",\"rank\":%d,\"plans\":%zu,\"bad\":%ld}\n", r, co.num_plans(), bad);
+    std::printf("{\"mode\":\"%s\",\"rank\":%d,\"plans\":%zu,\"puts\":%zu,\"bad\":%ld}\n",
+                bulk ? "bulk" : "structured", r, co.num_plans(), bco.num_puts(), bad);
     (void)hipFree(dd);
     (void)hipFree(df);
     return bad;
 }
 
-int loopback(int px, int py, int pz, int N, int H, bool pipelined = false)
+int loopback(int px, int py, int pz, int N, int H, bool pipelined = false, bool bulk = false)
 {
     const int n = px * py * pz;
     loopback_hub hub(n);
@@ -129,7 +143,7 @@ int loopback(int px, int py, int pz, int N, int H, bool pipelined = false)
             {
                 communication_object::options opt;
                 opt.pipelined = pipelined;
-                bad += run_structured_rank(ts[std::size_t(r)], {px, py, pz}, N, H, opt);
+                bad += run_structured_rank(ts[std::size_t(r)], {px, py, pz}, N, H, opt, 2, bulk);
             }
             catch (const std::exception& e)
             {
@@ -281,6 +295,9 @@ int main(int argc, char** argv)
         if (mode == "pipeloop" && argc == 7)
             return loopback(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
                             std::atoi(argv[6]), true);
+        if (mode == "bulkloop" && argc == 7)
+            return loopback(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                            std::atoi(argv[6]), false, true);
         if (mode == "rccl" && argc == 5) return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
         if (mode == "rccl" && argc == 6)
             return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]));

@@ -138,3 +138,32 @@ def test_co_rccl_pipelined(self_tr):
     rc, lines, err = _run(["rccl", 12, 2, self_tr, 1])
     assert rc == 0, (lines, err)
     assert all(l.get("bad", 1) == 0 for l in lines if l.get("mode") == "structured")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,N,H", [((1, 1, 1), 12, 2), ((2, 1, 1), 10, 2), ((2, 2, 2), 8, 3),
+                                       ((3, 1, 2), 7, 2), ((1, 2, 2), 9, 1)])
+def test_co_bulk_loopback(parts, N, H):
+    """The C++ bulk_communication_object (zero-copy puts, include/ghex_amd/
+    bulk_communication_object.hpp): ranks as threads, two fields (double, float) registered
+    with add_field, init, two exchanges; every cell of every rank."""
+    rc, lines, err = _run(["bulkloop", *parts, N, H])
+    ranks = [l for l in lines if l.get("mode") == "bulk"]
+    assert rc == 0, (lines, err)
+    assert len(ranks) == parts[0] * parts[1] * parts[2]
+    assert all(l["bad"] == 0 and l["puts"] >= 1 and l["plans"] == 0 for l in ranks)
+
+
+def test_bulk_header_compiles_host_only(tmp_path):
+    """The bulk header is plain host C++ too."""
+    src = tmp_path / "b.cpp"
+    src.write_text(
+        '#include <ghex_amd/bulk_communication_object.hpp>\n'
+        '#include <ghex_amd/field_descriptor.hpp>\n'
+        'int main(){ ghex_amd::bulk_handle h; h.wait(); return h.is_ready() ? 0 : 1; }\n')
+    exe = tmp_path / "b"
+    subprocess.run(["g++", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", INC, "-I",
+                    "/opt/rocm/include", str(src), "-o", str(exe), "-L", LIB, "-lghx",
+                    "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{LIB}",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    assert subprocess.run([str(exe)]).returncode == 0
