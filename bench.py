@@ -370,11 +370,12 @@ def main():
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            # (profiled on the one-domain plan: N=1 only; per-peer buffers at N>1)
-            ent = tj.get(f"N{N}_H{Hw}", {}).get(dom_name) if world == 1 else None
+            # N=1: the one-domain plan; N>1: rank 0's plan of the same decomposition (every rank's
+            # plan is a translate of it), profiled on one GPU through tools/emu_rank_bench.py
+            ent = tj.get(f"N{N}_H{Hw}" + ("" if world == 1 else f"_w{world}"), {}).get(dom_name)
             if ent:
                 traffic = ent.get("hbm_bytes_per_launch")
-                traffic_src = tj.get("source")
+                traffic_src = ent.get("source", tj.get("source"))
         except Exception:
             traffic = None
     out["roofline"] = {
