@@ -51,8 +51,9 @@ def parse():
     p.add_argument("--N", type=int, default=512)
     p.add_argument("--halo", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph")
-    p.add_argument("--steps-per-graph", type=int, default=10,
-                   help="steps captured per hipGraph (the K timed steps replay K/G graphs)")
+    p.add_argument("--steps-per-graph", type=int, default=0,
+                   help="steps captured per hipGraph (the K timed steps replay K/G graphs); "
+                        "0: all K steps in one graph (at most 1000)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true")
@@ -286,7 +287,8 @@ def main():
         unpack(s)
 
     K, W = args.steps, args.warmup
-    runner = Runner(torch, dev, stream, step, args.steps_per_graph, eager=args.no_graph)
+    G = args.steps_per_graph or min(K, 1000)
+    runner = Runner(torch, dev, stream, step, G, eager=args.no_graph)
     runner.prepare(W)
     runner.prepare(K)
     runner.run(W)
@@ -329,8 +331,8 @@ def main():
                         f"device-resident pack+unpack, decomposition {list(parts)}",
             "N": N, "halo": Hw, "fields": 1, "decomposition": list(parts),
             "launch": ("eager" if args.no_graph else
-                       f"hipGraphs of {args.steps_per_graph} steps, instantiated before the "
-                       "timed region") + ", pack launch + unpack launch per step",
+                       f"hipGraphs of {G} steps, instantiated before the timed region") +
+                      ", pack launch + unpack launch per step",
             "bytes_per_step_per_gpu": step_bytes,
             "parallelism": f"{world} rank(s), one domain per GPU",
             "world_size": world, "backend": backend,
@@ -729,7 +731,7 @@ def bench_halo(h, v, torch, dist, dev, stream, args):
         pack(s)
         unpack(s)
     K = min(v["K"], 100)
-    runner = Runner(torch, dev, stream, step, args.steps_per_graph, eager=args.no_graph)
+    runner = Runner(torch, dev, stream, step, args.steps_per_graph or K, eager=args.no_graph)
     runner.prepare(K)
     runner.run(K)
     T = v["timed"](lambda: runner.run(K), 1)
