@@ -74,7 +74,11 @@ def main(rn):
     with open(os.path.join(dst, f"{rn}_pmc.json"), "w") as fh:
         json.dump(pmc, fh, indent=1)
     traffic["source"] = f"profiles/{rn}_pmc.json (rocprofv3 --pmc, tools/pmc.sh)"
-    with open(os.path.join(dst, "pmc_traffic.json"), "w") as fh:
+    tp = os.path.join(dst, "pmc_traffic.json")
+    if os.path.exists(tp):  # keep the per-rank-plan entries (N512_H2_w*, tools/pmc_emu.sh)
+        old = json.load(open(tp))
+        traffic = {**{k: v for k, v in old.items() if "_w" in k}, **traffic}
+    with open(tp, "w") as fh:
         json.dump(traffic, fh, indent=1)
     print("collected", rn)
 
