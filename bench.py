@@ -523,6 +523,10 @@ def extras(args, torch, dist, dev, stream, out, v):
     # the north star's other halo widths, same decomposition, same two-launch step, verified
     out["halo_widths"] = {str(h): bench_halo(h, v, torch, dist, dev, stream, args)
                           for h in (1, 3) if h != Hw}
+    if world == 1 and N == 512 and Hw == 2:
+        # the same cells and bytes in a field whose x rows are allocated 2 cells wider (row pitch
+        # 4,144 B instead of 4,128 B): what the x-face lines' address set costs
+        out["layout_x_alloc_518"] = bench_halo(Hw, v, torch, dist, dev, stream, args, x_alloc=518)
     if world == 1 or args.bulk:
         # zero-copy bulk exchange (BulkCommunicationObject): puts straight into the
         # receivers' halos, no buffers: 2*n*8 bytes moved per step (not the metric's 4*n*8)
@@ -685,9 +689,10 @@ def kernel_durations(torch, dev, stream, fns, M=10, rounds=31):
     return tuple(out)
 
 
-def bench_halo(h, v, torch, dist, dev, stream, args):
+def bench_halo(h, v, torch, dist, dev, stream, args, x_alloc=None):
     """The headline's step (pack launch + unpack launch, hipGraphs instantiated beforehand) for
-    halo width h on the same decomposition, after a verified full exchange; one dict."""
+    halo width h on the same decomposition, after a verified full exchange; one dict. x_alloc:
+    allocate the field's x rows this many cells wide (the logical field is its first N+2h)."""
     N, world, rank, R, _ghx, L = v["N"], v["world"], v["rank"], v["R"], v["_ghx"], v["L"]
     parts = DECOMP[world]
     G = [parts[d] * N for d in range(3)]
@@ -698,7 +703,8 @@ def bench_halo(h, v, torch, dist, dev, stream, args):
     dd = R.DomainDescriptor(rank, first, last)
     pc = R.make_pattern(v["ctx"], R.HaloGenerator((0, 0, 0), tuple(g - 1 for g in G), (h,) * 6,
                                                   (True,) * 3), [dd])
-    base = torch.full((E, E, E), -1.0, dtype=torch.float64, device=dev)
+    alloc = torch.full((E, E, x_alloc or E), -1.0, dtype=torch.float64, device=dev)
+    base = alloc[:, :, :E]
     ar = [torch.arange(N, device=dev, dtype=torch.float64) + first[d] for d in range(3)]
     base[h:h + N, h:h + N, h:h + N] = (
         ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)))
@@ -743,7 +749,9 @@ def bench_halo(h, v, torch, dist, dev, stream, args):
            "unpack_us": round(t_u * 1e6, 2), "pack_kernel_us": round(k_p * 1e6, 2),
            "unpack_kernel_us": round(k_u * 1e6, 2), "bytes_per_step_per_gpu": 4 * n * 8,
            "verified": bad == 0}
-    del runner, co, base, fd, bis, send, recv
+    if x_alloc:
+        out["row_pitch_bytes"] = 8 * x_alloc
+    del runner, co, base, alloc, fd, bis, send, recv
     torch.cuda.empty_cache()
     return out
 
