@@ -504,6 +504,29 @@ def extras(args, torch, dist, dev, stream, out, v):
         co.exchange(bis).wait()
     Te = timed(lambda: co.exchange(bis).wait(), ke)
     out["exchange_ms_per_step"] = round(Te / ke * 1e3, 4)
+    if world > 1 and not args.rehearse:
+        # the transport alone: the same peer messages as one RCCL group per step, no pack or
+        # unpack (what exchange_ms_per_step adds to the two kernels)
+        from ghex_amd.communication_object import route
+        me = rank
+        tsends = [(x["rank"], x["tag"], send[i][:x["size"]]) for i, x in enumerate(plan.send)
+                  if x["rank"] != me]
+        trecvs = [(x["rank"], x["tag"], recv[i][:x["size"]]) for i, x in enumerate(plan.recv)
+                  if x["rank"] != me]
+
+        def transport_only():
+            for w in route(v["ctx"], tsends, trecvs):
+                w.wait()
+            torch.cuda.current_stream(dev).synchronize()
+        try:
+            for _ in range(3):
+                transport_only()
+            Tt = timed(transport_only, ke)
+            out["transport_ms_per_step"] = round(Tt / ke * 1e3, 4)
+            out["transport_bytes_per_step_per_gpu"] = sum(t.numel() for _, _, t in tsends)
+        except Exception as e:  # reported; the legs after it still run
+            out["transport_error"] = f"{type(e).__name__}: {str(e)[:200]}"
+        co.exchange(bis).wait()  # halos valid again (the recv buffers were overwritten)
     if world > 1:
         # per-peer streams (rehearsal: the host-staged form of the same pipeline over gloo)
         cop = R.make_communication_object(v["ctx"], pipelined=True,
