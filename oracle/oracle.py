@@ -91,6 +91,12 @@ class Box2:
         return s
 
 
+def _cmod(a: int, b: int) -> int:
+    """C/C++ integer remainder (truncating division): the sign follows the dividend."""
+    r = abs(a) % abs(b)
+    return -r if a < 0 else r
+
+
 def regular_halo_boxes(gfirst, glast, halos, periodic, dfirst, dlast) -> List[Box2]:
     """halo_generator::operator() (halo_generator.hpp:93-148).
 
@@ -133,7 +139,9 @@ def regular_halo_boxes(gfirst, glast, halos, periodic, dfirst, dlast) -> List[Bo
             ext_h = gl[d] - gf[d]
             ext = glast[d] + 1 - gfirst[d]
             off = gf[d] - gfirst[d]
-            gf[d] = (off + ext) % ext + gfirst[d]
+            # C++ `%` truncates toward zero: a box starting more than one period before the
+            # domain keeps a negative offset (halo_generator.hpp:139-141), unlike Python's `%`
+            gf[d] = _cmod(off + ext, ext) + gfirst[d]
             gl[d] = gf[d] + ext_h
         b.gf, b.gl = tuple(gf), tuple(gl)
     return out

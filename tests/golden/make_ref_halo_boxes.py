@@ -94,6 +94,21 @@ def configs():
             out.append(dict(D=3, gfirst=[0, 0, 0], glast=[47, 23, 15], halos=[2, 1, 1, 2, 1, 1],
                             periodic=list(periodic), dom=list(map(list, doms[di])),
                             others=[list(map(list, o)) for o in doms]))
+    # halos wider than a domain and wider than the whole periodic extent (the wrap of a box that
+    # starts more than one period before the domain: C++ truncating %, halo_generator.hpp:139-141)
+    for gsize, parts, halos in [((8, 2, 2), (4, 1, 1), (3,) * 6), ((3, 3, 3), (3, 3, 3), (2,) * 6),
+                                ((5, 2, 1), (5, 2, 1), (2,) * 6), ((8, 4, 4), (4, 2, 2), (3,) * 6),
+                                ((4, 4, 4), (1, 1, 1), (5, 9, 1, 4, 6, 2))]:
+        doms = decompose(gsize, parts)
+        for periodic in [(1, 1, 1), (1, 0, 1)]:
+            for di in range(min(len(doms), 4)):
+                out.append(dict(D=3, gfirst=[0, 0, 0], glast=[g - 1 for g in gsize],
+                                halos=list(halos), periodic=list(periodic),
+                                dom=list(map(list, doms[di])),
+                                others=[list(map(list, o)) for o in doms]))
+    for halos in [(5, 2), (7, 7)]:
+        out.append(dict(D=1, gfirst=[0], glast=[2], halos=list(halos), periodic=[1],
+                        dom=[[0], [2]], others=[[[0], [2]]]))
     # the bench geometry at 512^3, H=1..3 (boxes only + the 2x2x2 split)
     for H in (1, 2, 3):
         out.append(dict(D=3, gfirst=[0, 0, 0], glast=[511, 511, 511], halos=[H] * 6,
