@@ -302,7 +302,7 @@ class CommunicationObject:
         :271-285): pack, transport, unpack are stream-ordered; wait() blocks the host."""
         import torch
         bis = self._as_list(buffer_infos)
-        stream = torch.cuda.current_stream(bis[0].field.device) if bis else None
+        stream = torch.cuda.current_stream(bis[0].field.device.index) if bis else None
         return self._start(bis, stream)
 
     def schedule_exchange(self, stream, *buffer_infos) -> CommunicationHandle:
@@ -314,6 +314,16 @@ class CommunicationObject:
         if stream is None and bis:
             stream = torch.cuda.current_stream(bis[0].field.device)
         return self._start(bis, stream)
+
+    def _done_event(self, stream):
+        """The completion event of the exchange being started, recorded on `stream`. One event per
+        object suffices: an exchange cannot start before the previous one completed."""
+        import torch
+        ev = self.__dict__.get("_ev")
+        if ev is None:
+            ev = self._ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
 
     def _start(self, bis, stream) -> CommunicationHandle:
         import torch
@@ -346,17 +356,15 @@ class CommunicationObject:
                 pl = self._pipeline_of(plan, device)
                 _ghx.call("ghx_pipeline_run", pl.h, fptrs, len(bis), sptrs, len(send), rptrs,
                           len(recv), stream.cuda_stream)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            return CommunicationHandle(self, stream, ev)
+            return CommunicationHandle(self, stream, self._done_event(stream))
         if self.fuse_self and self.all_self(plan):
             # every message stays on this device: pack + unpack in one launch (the launch and
             # the event go to `stream` explicitly: no current-stream switch needed)
-            _ghx.call("ghx_exchange_self", plan.h, fptrs, len(bis), sptrs, len(send),
-                      stream.cuda_stream)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            return CommunicationHandle(self, stream, ev)
+            rc = _ghx.lib().ghx_exchange_self(plan.h, fptrs, len(bis), sptrs, len(send),
+                                              stream.cuda_stream)
+            if rc:
+                _ghx.check(rc, "ghx_exchange_self")
+            return CommunicationHandle(self, stream, self._done_event(stream))
         with torch.cuda.stream(stream):
             mixed = self.fuse_self and self.mixed(plan)
             _ghx.call("ghx_exchange_pack_self" if mixed else "ghx_exchange_pack", plan.h,
@@ -373,8 +381,7 @@ class CommunicationObject:
                     w.wait()  # NCCL: the stream waits for the recvs, the host does not
             _ghx.call("ghx_exchange_unpack_peers" if mixed else "ghx_exchange_unpack",
                       plan.h, fptrs, len(bis), rptrs, len(recv), stream.cuda_stream)
-            ev = torch.cuda.Event()
-            ev.record(stream)
+            ev = self._done_event(stream)
         return CommunicationHandle(self, stream, ev)
 
     def _host_buffers(self, plan, sends, recvs):
