@@ -287,8 +287,8 @@ def main():
         unpack(s)
 
     K, W = args.steps, args.warmup
-    G = args.steps_per_graph or min(K, 1000)
-    runner = Runner(torch, dev, stream, step, G, eager=args.no_graph)
+    spg = args.steps_per_graph or min(K, 1000)  # steps per hipGraph
+    runner = Runner(torch, dev, stream, step, spg, eager=args.no_graph)
     runner.prepare(W)
     runner.prepare(K)
     runner.run(W)
@@ -331,7 +331,7 @@ def main():
                         f"device-resident pack+unpack, decomposition {list(parts)}",
             "N": N, "halo": Hw, "fields": 1, "decomposition": list(parts),
             "launch": ("eager" if args.no_graph else
-                       f"hipGraphs of {G} steps, instantiated before the timed region") +
+                       f"hipGraphs of {spg} steps, instantiated before the timed region") +
                       ", pack launch + unpack launch per step",
             "bytes_per_step_per_gpu": step_bytes,
             "parallelism": f"{world} rank(s), one domain per GPU",
@@ -425,7 +425,9 @@ def main():
     try:
         extras(args, torch, dist, dev, stream, out, locals())
     except Exception as e:  # reported, never fatal for the headline measurement
+        import traceback
         out["extras_error"] = f"{type(e).__name__}: {str(e)[:300]}"
+        out["extras_traceback"] = traceback.format_exc()[-1200:]
     extras_done.set()
     emit(out)
     sys.stdout.flush()
