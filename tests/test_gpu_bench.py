@@ -39,7 +39,10 @@ def test_bench_line_n1_small():
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["launch_us"] > 0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["algorithmic_bytes_per_launch"] == 2 * (68 ** 3 - 64 ** 3) * 8
-    assert "cold_clean_launch_us" in r and "fused_self" in d
+    assert "cold_clean_launch_us" in r and "cold_clean_step_us" in r and "fused_self" in d
+    # the dominant launch's share of the step comes from the kernels' own start/stop events
+    assert r["pack_kernel_us"] > 0 and r["unpack_kernel_us"] > 0
+    assert r["launch_us"] <= r["step_device_us"]
     assert d["fused_self"]["bytes_moved"] == 3 * (68 ** 3 - 64 ** 3) * 8
     assert "extras_error" not in d, d.get("extras_error")
 
