@@ -498,6 +498,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 1) throw invalid("mixed_always must be 0 or 1");
             g_tune.mixed_always = value;
         }
+        else if (k == "xcd_rotate")
+        {
+            if (value < 0 || value > 1) throw invalid("xcd_rotate must be 0 or 1");
+            g_tune.xcd_rotate = value;
+        }
         else if (k == "lds")
         {
             if (value < 0 || value > 1) throw invalid("lds must be 0 or 1");

@@ -74,6 +74,8 @@ struct tuning
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt
                                        // round-robin over the 8 XCDs) at the same time
+    int xcd_rotate = 0;                // line-sharing pair groups dealt to the XCDs rotated by
+                                       // the group index (balances the L2 channels per XCD)
     int lds = 0;                       // 1: pack 8/16-B rows through LDS (copy_tile_lds:
                                        // whole 64-B blocks read four lanes each, pieces
                                        // extracted one row per lane)

@@ -146,10 +146,15 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
             for (size_t k = 0; k < n; k += 8)
             {
                 const size_t m = std::min<size_t>(8, n - k);
-                for (size_t u = 0; u < m; ++u) emit(uint32_t(j), per[size_t(j)][k + u]);
+                // xcd_rotate: group g deals its tiles to the XCDs rotated by g, so an XCD's tiles
+                // come from every residue of the tile index (the L2 channel a line maps to varies
+                // with high address bits: with tiles dealt in plain order each XCD would see the
+                // same few channels over and over)
+                const size_t rot = g_tune.xcd_rotate ? (k / 8) % m : 0;
+                for (size_t u = 0; u < m; ++u) emit(uint32_t(j), per[size_t(j)][k + (u + rot) % m]);
                 for (size_t u = m; u < 8 && next < rest.size(); ++u, ++next)
                     emit(rest[next].first, rest[next].second);
-                for (size_t u = 0; u < m; ++u) emit(i, per[i][k + u]);
+                for (size_t u = 0; u < m; ++u) emit(i, per[i][k + (u + rot) % m]);
             }
         }
         for (; next < rest.size(); ++next) emit(rest[next].first, rest[next].second);

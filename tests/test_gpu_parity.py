@@ -406,7 +406,8 @@ def test_full_size_512_h2_checksum():
                                    {"grid_cap": 7, "nt": 1}, {"short_pol": 3},
                                    {"short_pol": 1, "small_row_bytes": 4096},
                                    {"short_xcds": 3, "small_tile_rows": 64},
-                                   {"lds": 1}, {"lds": 1, "small_tile_rows": 100}],
+                                   {"lds": 1}, {"lds": 1, "small_tile_rows": 100},
+                                   {"xcd_rotate": 1, "small_tile_rows": 64}],
                          ids=lambda d: "-".join(f"{k}={v}" for k, v in d.items()))
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_tuning_variants_stay_bit_exact(knobs, Hw):
