@@ -123,6 +123,13 @@ def test_structured_exchange_gloo(world, parts, Hw):
     _run(world, _structured_exchange_worker, parts, Hw, 6)
 
 
+def test_config1_128cube_two_ranks_gloo():
+    """BASELINE config 1 at its full size (the reference's CPU-runnable case,
+    benchmarks/simple_comm_test_halo_exchange_3D_generic_full.cpp): 128^3 fp64 per rank, H=1,
+    periodic, (2,1,1) over 2 gloo ranks — product planning and routing, oracle bytes, every cell."""
+    _run(2, _structured_exchange_worker, (2, 1, 1), 1, 128)
+
+
 def _unstructured_worker(rank, world, case):
     import ghex_amd
     from ghex_amd.communication_object import route

@@ -217,6 +217,12 @@ def test_halo_wider_than_neighbour_domains(parts, N, Hw):
     _cube_multi_rank(parts, N, Hw, full=False)
 
 
+def test_config1_full_size_two_emulated_ranks():
+    """BASELINE config 1 (128^3 fp64 per rank, H=1, periodic, (2,1,1)) on the device path: both
+    ranks' packed buffers routed, unpacked, every cell equal to the oracle's exchange."""
+    _cube_multi_rank((2, 1, 1), 128, 1)
+
+
 def _cube_multi_rank(parts, N, Hw, mixed=False, full=True):
     from ghex_amd.structured import regular as R
     from tests.gpu_util import FakeContext, device_field, emulated_exchange
