@@ -358,6 +358,10 @@ def main():
     k_pack, k_unpack = launch_durations(torch, dev, stream, _ghx, [pack, unpack])
     if min(k_pack, k_unpack) <= 0:
         k_pack, k_unpack = t_pack, t_unpack
+    if distributed:  # the slowest rank's figures (the line is rank 0's)
+        dev_step = all_reduce_host(dev_step, dist.ReduceOp.MAX)
+        k_pack = all_reduce_host(k_pack, dist.ReduceOp.MAX)
+        k_unpack = all_reduce_host(k_unpack, dist.ReduceOp.MAX)
     dom_name, dom_d = ("pack", t_pack) if k_pack >= k_unpack else ("unpack", t_unpack)
     dom_k = max(k_pack, k_unpack)
     # the dominant launch's share of the timed region's device time (HIP events around the K
