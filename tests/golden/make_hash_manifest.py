@@ -8,7 +8,9 @@ Run in the build container:  python tests/golden/make_hash_manifest.py [--no-ful
 Cases (all periodic, cube_domains geometry, owned cell = global linear index, halos -1):
   small: N in {8, 13} x H in {1, 2, 3} x the 6 layout maps x decompositions 1, (2,1,1), (2,2,2)
   asym : N=8, field offset 2, halos {0,0,1,0,1,2} (test_regular_domain.cpp pattern 1), (2,1,1)
-  full : 512^3 fp64 H in {1, 2, 3} on one rank (BASELINE config 2), and 2x2x2 at N=64 H=2
+  full : 512^3 fp64 H in {1, 2, 3} on one rank (BASELINE config 2), 2x2x2 at N=64 H=2, and
+         2x2x2 ranks of 512^3 H=2 (BASELINE config 3 at full size; ~15 GB of host memory)
+  --only NAME updates one full case in the existing manifest.
 The GPU tests recompute the same checksums from the HIP path (tests/test_gpu_manifest.py);
 tests/test_oracle.py re-derives the small cases from the oracle (regression pin)."""
 import json
@@ -65,6 +67,7 @@ def full_cases():
     for Hw in (1, 2, 3):
         yield (512, Hw, (2, 1, 0), (1, 1, 1), None)
     yield (64, 2, (2, 1, 0), (2, 2, 2), None)
+    yield (512, 2, (2, 1, 0), (2, 2, 2), None)
 
 
 def main(full=True):
@@ -81,5 +84,18 @@ def main(full=True):
         json.dump(out, fh, indent=0, sort_keys=True)
 
 
+def update_one(name):
+    path = os.path.join(HERE, "hash_manifest.json")
+    out = json.load(open(path))
+    case = next(c for c in full_cases() if case_name(*c) == name)
+    out["full"][name] = run_case(*case)
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=0, sort_keys=True)
+    print("updated", name)
+
+
 if __name__ == "__main__":
-    main(full="--no-full" not in sys.argv)
+    if "--only" in sys.argv:
+        update_one(sys.argv[sys.argv.index("--only") + 1])
+    else:
+        main(full="--no-full" not in sys.argv)

@@ -2,7 +2,7 @@
 tests/golden/make_hash_manifest.py from the oracle): every packed message and every field after
 unpack, FNV-1a 64, for 109 small cases (2 cube sizes x 3 halos x 6 layout maps x 3
 decompositions + asymmetric halos) and the full-size cases (512^3 fp64 H=1/2/3 on one rank —
-BASELINE config 2 — and 2x2x2 ranks of 64^3). Multi-rank cases are emulated in one process
+BASELINE config 2 — 2x2x2 ranks of 64^3, and 2x2x2 ranks of 512^3 H=2 — BASELINE config 3). Multi-rank cases are emulated in one process
 (tests/gpu_util.emulated_exchange); single-rank cases run the communication object's own
 exchange(), i.e. the fused self-exchange kernel the bench measures."""
 import json
@@ -36,6 +36,19 @@ def _parse(name):
             tuple(int(c) for c in parts["P"]), halos)
 
 
+def _device_linear_field(dom, N, Hw, gl):
+    """helpers.linear_index_field for layout (2,1,0), built on the device (full sizes): owned cell
+    = global linear index x + Gx*(y + Gy*z), halos -1; memory order (z, y, x)."""
+    import torch
+    E = N + 2 * Hw
+    G = [g + 1 for g in gl]
+    base = torch.full((E, E, E), -1.0, dtype=torch.float64, device="cuda")
+    ar = [torch.arange(N, device="cuda", dtype=torch.float64) + dom.first[d] for d in range(3)]
+    base[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = (
+        ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)))
+    return base, base.permute(2, 1, 0)
+
+
 def gpu_case(N, Hw, layout, parts, halos=None):
     import torch
     from ghex_amd.structured import regular as R
@@ -50,9 +63,12 @@ def gpu_case(N, Hw, layout, parts, halos=None):
         ctx = FakeContext(r, nr, table)
         dd = R.DomainDescriptor(ranks[r][0].id, ranks[r][0].first, ranks[r][0].last)
         pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, halos, (1, 1, 1)), [dd])
-        a, _ = H.linear_index_field(ranks[r][0], N, Hw, gl, layout=layout)
-        base, logical = device_field(a, layout)
-        del a
+        if N >= 256 and layout == (2, 1, 0):
+            base, logical = _device_linear_field(ranks[r][0], N, Hw, gl)
+        else:
+            a, _ = H.linear_index_field(ranks[r][0], N, Hw, gl, layout=layout)
+            base, logical = device_field(a, layout)
+            del a
         fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (E,) * 3)
         cos.append(R.make_communication_object(ctx))
         bis.append([pc(fd)])
