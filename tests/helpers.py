@@ -82,7 +82,7 @@ def cube_domains(N, parts):
     return ranks, (0, 0, 0), g_last
 
 
-def linear_index_field(dom, N, H, g_last, dtype=np.float64, layout=(2, 1, 0), seed=None):
+def linear_index_field(dom, N, H, g_last, dtype=np.float64, layout=(2, 1, 0), seed=None, add=0):
     """Cube field of extent (N+2H)^3, owned cells = global linear index (exact in fp64 < 2^53),
     halos pre-filled with -1 (SURVEY §8(d) synthetic inputs). Returns (array, FieldSpec).
 
@@ -100,7 +100,8 @@ def linear_index_field(dom, N, H, g_last, dtype=np.float64, layout=(2, 1, 0), se
     val = coords[0] + gx * (coords[1] + gy * coords[2])
     if seed is not None:
         val = (val * 2654435761 + seed) % (1 << 40)
-    a[tuple(slice(H, H + N) for _ in order)] = val.astype(dtype)
+    val = val + add  # per-field offset (BASELINE config 4: field number)
+    a[tuple(slice(H, H + N) for _ in order)] = val.astype(np.float64).astype(dtype)
     spec = orc.FieldSpec(a, a.itemsize, tuple(layout), (H, H, H), (E, E, E))
     return a, spec
 

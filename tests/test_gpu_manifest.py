@@ -106,3 +106,63 @@ def test_full_case_matches_manifest(name):
     assert got["messages"] == exp["messages"]
     assert got["fields"] == exp["fields"]
     torch.cuda.empty_cache()
+
+
+C4_TYPES = ["float64", "float32", "float64", "float32", "float64"]
+
+
+def _device_c4_field(dom, N, Hw, gl, dtype, add):
+    """helpers.linear_index_field(dtype, add) built on the device: owned = global linear index +
+    add (computed in f64, rounded once to dtype), halos -1; memory order (z, y, x)."""
+    import torch
+    E = N + 2 * Hw
+    G = [g + 1 for g in gl]
+    T = getattr(torch, dtype)
+    base = torch.full((E, E, E), -1, dtype=T, device="cuda")
+    ar = [torch.arange(N, device="cuda", dtype=torch.float64) + dom.first[d] for d in range(3)]
+    base[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = (
+        ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)) + add
+    ).to(T)
+    return base, base.permute(2, 1, 0)
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST.get("config4", {})))
+def test_config4_five_fields_matches_manifest(name):
+    """BASELINE config 4 (five fields [f64, f32, f64, f32, f64], H=3, 2x2x2, ONE exchange per
+    rank): every packed message (pads zero on both sides) and every field after unpack."""
+    import torch
+    from ghex_amd.structured import regular as R
+    from tests.gpu_util import FakeContext, emulated_exchange
+    p = dict((q[0], q[1:]) for q in name.split("_")[1:])
+    N, Hw, parts = int(p["N"]), int(p["H"]), tuple(int(c) for c in p["P"])
+    ranks, gf, gl = H.cube_domains(N, parts)
+    nr = len(ranks)
+    table = {r: [(d.id, d.first, d.last) for d in ranks[r]] for r in range(nr)}
+    cos, bis, bases = [], [], []
+    for r in range(nr):
+        ctx = FakeContext(r, nr, table)
+        dd = R.DomainDescriptor(ranks[r][0].id, ranks[r][0].first, ranks[r][0].last)
+        pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (1, 1, 1)), [dd])
+        bl = []
+        for k, T in enumerate(C4_TYPES):
+            base, logical = _device_c4_field(ranks[r][0], N, Hw, gl, T, k)
+            bl.append(pc(R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)))
+            bases.append(base)
+        co = R.make_communication_object(ctx)
+        for t in co.buffers(co.plan(bl), torch.device("cuda", 0))[0]:
+            t.zero_()  # pad bytes are never written by the pack: zero, as in the oracle
+        cos.append(co)
+        bis.append(bl)
+    plans, bufs = emulated_exchange(cos, bis)
+    torch.cuda.synchronize()
+    exp = MANIFEST["config4"][name]
+    msgs = {}
+    for r in range(nr):
+        for i, x in enumerate(plans[r].send):
+            b = bufs[r][0][i][:x["size"]].cpu().numpy()
+            msgs[f"{r}:{x['pair'][0]},{x['pair'][1]}"] = [int(x["size"]),
+                                                          f"{orc.fnv1a64(b):016x}"]
+    assert msgs == exp["messages"]
+    assert [f"{orc.fnv1a64(b.cpu().numpy()):016x}" for b in bases] == exp["fields"]
+    del bases
+    torch.cuda.empty_cache()
