@@ -500,7 +500,7 @@ int ghx_tune(const char* key, int32_t value)
         }
         else if (k == "xcd_rotate")
         {
-            if (value < 0 || value > 1) throw invalid("xcd_rotate must be 0 or 1");
+            if (value < 0 || value > 2) throw invalid("xcd_rotate must be 0, 1 or 2");
             g_tune.xcd_rotate = value;
         }
         else if (k == "lds")

@@ -150,11 +150,23 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
                 // come from every residue of the tile index (the L2 channel a line maps to varies
                 // with high address bits: with tiles dealt in plain order each XCD would see the
                 // same few channels over and over)
-                const size_t rot = g_tune.xcd_rotate ? (k / 8) % m : 0;
-                for (size_t u = 0; u < m; ++u) emit(uint32_t(j), per[size_t(j)][k + (u + rot) % m]);
+                size_t pos[8];
+                for (size_t u = 0; u < m; ++u) pos[u] = g_tune.xcd_rotate == 1 ? (u + k / 8) % m : u;
+                if (g_tune.xcd_rotate == 2)  // a pseudo-random order per group (fixed seed)
+                {
+                    uint64_t x = 0x9e3779b97f4a7c15ull * (k / 8 + 1);
+                    for (size_t u = m; u > 1; --u)
+                    {
+                        x ^= x >> 33;
+                        x *= 0xff51afd7ed558ccdull;
+                        x ^= x >> 33;
+                        std::swap(pos[u - 1], pos[x % u]);
+                    }
+                }
+                for (size_t u = 0; u < m; ++u) emit(uint32_t(j), per[size_t(j)][k + pos[u]]);
                 for (size_t u = m; u < 8 && next < rest.size(); ++u, ++next)
                     emit(rest[next].first, rest[next].second);
-                for (size_t u = 0; u < m; ++u) emit(i, per[i][k + (u + rot) % m]);
+                for (size_t u = 0; u < m; ++u) emit(i, per[i][k + pos[u]]);
             }
         }
         for (; next < rest.size(); ++next) emit(rest[next].first, rest[next].second);

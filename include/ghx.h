@@ -53,8 +53,8 @@ typedef void* ghx_stream;
  * "short_pol" (field-side cache policy of short-row segments: bit 0 non-temporal loads,
  * bit 1 sc1 stores), "xcd_pair" (0|1: line-sharing short-row segment pairs dispatched in
  * lock-step groups of 8 tiles, same XCD), "short_xcds" (0..7: short-row tiles dealt to the
- * first this many XCDs only, 0 = all), "xcd_rotate" (0|1: pair groups dealt to the XCDs rotated
- * by the group index), "lds" (0|1: pack 8/16-B rows staged through LDS as
+ * first this many XCDs only, 0 = all), "xcd_rotate" (0|1|2: pair groups dealt to the XCDs in
+ * order, rotated by the group index, or in a pseudo-random order), "lds" (0|1: pack 8/16-B rows staged through LDS as
  * whole 64-B blocks), "urun" (0|1: run path for 4/8-B index-list rows),
  * "u_run_tile_rows" (rows per tile of run-heavy index lists); fused self exchange:
  * "self_tile_bytes", "self_lane_local" (0|1: pack->unpack hand-off inside each lane, no

@@ -413,7 +413,8 @@ def test_full_size_512_h2_checksum():
                                    {"short_pol": 1, "small_row_bytes": 4096},
                                    {"short_xcds": 3, "small_tile_rows": 64},
                                    {"lds": 1}, {"lds": 1, "small_tile_rows": 100},
-                                   {"xcd_rotate": 1, "small_tile_rows": 64}],
+                                   {"xcd_rotate": 1, "small_tile_rows": 64},
+                                   {"xcd_rotate": 2, "small_tile_rows": 64}],
                          ids=lambda d: "-".join(f"{k}={v}" for k, v in d.items()))
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_tuning_variants_stay_bit_exact(knobs, Hw):
