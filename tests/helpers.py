@@ -100,8 +100,9 @@ def linear_index_field(dom, N, H, g_last, dtype=np.float64, layout=(2, 1, 0), se
     val = coords[0] + gx * (coords[1] + gy * coords[2])
     if seed is not None:
         val = (val * 2654435761 + seed) % (1 << 40)
-    val = val + add  # per-field offset (BASELINE config 4: field number)
-    a[tuple(slice(H, H + N) for _ in order)] = val.astype(np.float64).astype(dtype)
+    if add:  # per-field offset (BASELINE config 4: field number), rounded once from f64
+        val = (val + add).astype(np.float64)
+    a[tuple(slice(H, H + N) for _ in order)] = val.astype(dtype)
     spec = orc.FieldSpec(a, a.itemsize, tuple(layout), (H, H, H), (E, E, E))
     return a, spec
 
