@@ -549,6 +549,13 @@ def extras(args, torch, dist, dev, stream, out, v):
                                               "one RCCL group on the pair's own communicator") +
                                              " and unpack of each peer's buffers on its stream"}
         del cop
+    if world > 1:
+        # the unstructured path between real ranks (BASELINE config 5's shape, scaled to 1M cells
+        # per rank so the setup all-gather stays small): verified and timed
+        try:
+            out["unstructured_exchange"] = bench_unstructured(v, torch, dist, dev, args)
+        except Exception as e:  # reported; the legs after it still run
+            out["unstructured_exchange"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
     # the north star's other halo widths, same decomposition, same two-launch step, verified
     out["halo_widths"] = {str(h): bench_halo(h, v, torch, dist, dev, stream, args)
                           for h in (1, 3) if h != Hw}
@@ -716,6 +723,56 @@ def kernel_durations(torch, dev, stream, fns, M=10, rounds=31):
         d = sorted(times[i + 1][r] - times[i][r] for r in range(rounds))
         out.append(d[len(d) // 2])
     return tuple(out)
+
+
+def bench_unstructured(v, torch, dist, dev, args, cells=1_000_000, frac=20):
+    """BASELINE config 5 between the real ranks, scaled: every rank owns `cells` cells (gids
+    rank*10^7 + i) and holds cells/frac halo cells drawn from the other ranks' (seed 20260715 +
+    rank), in a randomly permuted local storage order; value = gid*100 (levels 1, fp64). One
+    CommunicationObject.exchange per step over the context's transport (RCCL; gloo + host staging
+    in a rehearsal); every halo value checked; bytes per rank and step 4 * halo * 8."""
+    import numpy as np
+    from ghex_amd import unstructured as U
+    rank, world, ctx, K = v["rank"], v["world"], v["ctx"], v["K"]
+    rng = np.random.default_rng(20260715 + rank)
+    nh = cells // frac
+    others = np.array([r for r in range(world) if r != rank])
+    owner = others[rng.integers(0, len(others), size=4 * nh)]
+    local = rng.integers(0, cells, size=4 * nh)
+    halo = np.unique(owner.astype(np.int64) * 10_000_000 + local)
+    halo = rng.permutation(halo)[:nh]
+    gids = np.concatenate([rank * 10_000_000 + np.arange(cells, dtype=np.int64), halo])
+    perm = rng.permutation(len(gids))
+    gids = gids[perm]
+    outer = np.nonzero(perm >= cells)[0]  # storage positions of the halo cells
+    dd = U.DomainDescriptor(rank, gids.tolist(), outer.tolist())
+    pc = U.make_pattern(ctx, U.HaloGenerator(), [dd])
+    init = gids.astype(np.float64) * 100.0
+    init[outer] = -1.0
+    field = torch.from_numpy(init).to(dev)
+    fd = U.make_field_descriptor(dd, field)
+    co = U.make_communication_object(ctx, staging="host" if args.rehearse else None)
+    bis = [pc(fd)]
+    co.exchange(bis).wait()
+    got = field.cpu().numpy()
+    bad = int((got[outer] != gids[outer].astype(np.float64) * 100.0).sum())
+    if world > 1:
+        t = torch.tensor([float(bad)], dtype=torch.float64, device="cpu" if args.rehearse else dev)
+        dist.all_reduce(t)
+        bad = int(t.item())
+    ke = min(K, 50)
+    for _ in range(3):
+        co.exchange(bis).wait()
+    T = v["timed"](lambda: co.exchange(bis).wait(), ke)
+    nbytes = 4 * nh * 8
+    out = {"cells_per_rank": cells, "halo_cells_per_rank": nh, "peers": int(len(others)),
+           "ms_per_exchange": round(T / ke * 1e3, 4),
+           "GBps_per_rank_algorithmic": round(nbytes * ke / T / 1e9, 2),
+           "transport": "gloo + host staging (rehearsal)" if args.rehearse else "RCCL",
+           "verified": bad == 0}
+    del co, bis, fd, field
+    torch.cuda.empty_cache()
+    return out
 
 
 def bench_halo(h, v, torch, dist, dev, stream, args, x_alloc=None):

@@ -53,6 +53,7 @@ def test_bench_spawns_two_ranks_rehearsal():
     assert d["n_gpus"] == 2 and d["verified"] is True
     assert d["config"]["decomposition"] == [2, 1, 1] and d["config"]["world_size"] == 2
     assert d["exchange_pipelined"]["verified"] is True
+    assert d["unstructured_exchange"].get("verified") is True, d["unstructured_exchange"]
     assert "extras_error" not in d, d.get("extras_error")
 
 
