@@ -963,7 +963,8 @@ def bench_config4(torch, dev, ghex_amd, R):
     t2 = _time_graph(torch, dev, two)
     n = E ** 3 - N ** 3
     nbytes = 4 * n * (3 * 8 + 2 * 4)
-    return {"GBps": round(nbytes / t2 / 1e9, 1), "us_per_exchange": round(t2 * 1e6, 2),
+    return {"GBps": round(nbytes / t2 / 1e9, 1), "frac": round(nbytes / t2 / 1e9 / HBM_PEAK_GBS, 4),
+            "us_per_exchange": round(t2 * 1e6, 2),
             "bytes_per_exchange": nbytes, "verified": ok, "form": "pack launch + unpack launch",
             "fused_self": {"us_per_exchange": round(t * 1e6, 2),
                            "bytes_moved": 3 * n * (3 * 8 + 2 * 4)} if fusedp else None}
@@ -1014,7 +1015,8 @@ def bench_config5(torch, dev, _ghx, levels):
     L.ghx_uplan_destroy(hp)
     L.ghx_uplan_destroy(hu)
     nbytes = 4 * nh * levels * 8
-    return {"GBps": round(nbytes / t / 1e9, 1), "us_per_exchange": round(t * 1e6, 2),
+    return {"GBps": round(nbytes / t / 1e9, 1), "frac": round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4),
+            "us_per_exchange": round(t * 1e6, 2),
             "bytes_per_exchange": nbytes, "cells": n, "halo_cells": nh, "peers": 7,
             "index_bytes_per_exchange": 2 * nh * 4}
 
