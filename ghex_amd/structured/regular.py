@@ -337,6 +337,8 @@ def make_field_descriptor(domain_desc: DomainDescriptor, field, offsets, extents
     """make_field_descriptor(domain, field, offsets, extents)
     (bindings/python/src/ghex/structured/regular.py:66-107): the layout map is derived from the
     tensor's strides. Only device (GPU) fields: this package is the device hot path."""
+    from ..util import check_arch
+    check_arch(arch)
     return FieldDescriptor(domain_desc, field, offsets, extents)
 
 

@@ -147,6 +147,8 @@ class DataDescriptor:
 
 
 def make_field_descriptor(domain_desc: DomainDescriptor, field, *, arch=None):
+    from .util import check_arch
+    check_arch(arch)
     return DataDescriptor(domain_desc, field)
 
 

@@ -168,3 +168,17 @@ def test_reference_binding_index_set_signatures():
         UnitRange(0, 2)[2]
     with pytest.raises(ValueError):
         UnitRange(3, 2)
+
+
+def test_architecture_argument_like_the_reference_binding():
+    """make_field_descriptor(..., arch=Architecture.X) as in bindings/python/src/ghex/
+    structured/regular.py:66-98: GPU accepted, CPU refused (device path, no CPU fallback)."""
+    import torch
+    from ghex_amd.structured.regular import DomainDescriptor, make_field_descriptor
+    from ghex_amd.util import Architecture
+    dd = DomainDescriptor(0, (0, 0, 0), (3, 3, 3))
+    f = torch.zeros(6, 6, 6)
+    with pytest.raises(ValueError):
+        make_field_descriptor(dd, f, (1, 1, 1), (6, 6, 6), arch=Architecture.CPU)
+    with pytest.raises(TypeError):  # GPU requested, but the tensor is in host memory
+        make_field_descriptor(dd, f, (1, 1, 1), (6, 6, 6), arch=Architecture.GPU)
