@@ -152,8 +152,22 @@ class HaloGenerator:
         loc = (_ghx.Box * max(1, n.value))()
         glo = (_ghx.Box * max(1, n.value))()
         _ghx.call("ghx_regular_halo_boxes", *args, loc, glo, n.value, ctypes.byref(n))
-        return [(tuple(loc[i].first[:D]), tuple(loc[i].last[:D]), tuple(glo[i].first[:D]),
-                 tuple(glo[i].last[:D])) for i in range(n.value)]
+        return HaloBoxes((tuple(loc[i].first[:D]), tuple(loc[i].last[:D]),
+                          tuple(glo[i].first[:D]), tuple(glo[i].last[:D])) for i in range(n.value))
+
+
+class HaloBoxes(list):
+    """The receive boxes of a domain, [(local_first, local_last, global_first, global_last)] in
+    generation order; `.local` / `.global_` give them as ProductSets, the two halves of the
+    reference binding's HaloContainer (bindings/python/src/ghex/structured/regular.py:105-154)."""
+
+    @property
+    def local(self):
+        return [ProductSet.from_coords(b[0], b[1]) for b in self]
+
+    @property
+    def global_(self):
+        return [ProductSet.from_coords(b[2], b[3]) for b in self]
 
 
 def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[DomainDescriptor]):

@@ -164,6 +164,10 @@ def test_reference_binding_index_set_signatures():
     b = HaloGenerator((0, 0, 0), (11, 9, 7), (1, 0, 2, 2, 0, 3), (True, False, True))
     assert a.halos == b.halos and a.periodic == b.periodic
     assert a(dd) == b(DomainDescriptor(7, (3, 0, 2), (8, 4, 3))) and len(a(dd)) > 0
+    boxes = a(dd)
+    assert [(g.ranges[0].start, g[(-1, -1, -1)]) for g in boxes.global_] == \
+        [(gf[0], gl) for (_, _, gf, gl) in boxes]
+    assert [l.shape for l in boxes.local] == [g.shape for g in boxes.global_]
     with pytest.raises(IndexError):
         UnitRange(0, 2)[2]
     with pytest.raises(ValueError):
