@@ -30,6 +30,24 @@ def allocate(extents: Sequence[int], dtype, x_alloc: Optional[int] = None, devic
     return mem[:, :, :ex].permute(2, 1, 0)
 
 
+class _LocalContext:
+    """A one-rank context: the trial exchanges are self exchanges of this process only."""
+    distributed = None
+    group = None
+
+    def rank(self):
+        return 0
+
+    def size(self):
+        return 1
+
+    def all_gather_object(self, obj):
+        return [obj]
+
+    def global_rank(self, r):
+        return r
+
+
 def suggest_x_alloc(extents: Sequence[int], halo: int, dtype=None,
                     candidates: Optional[Iterable[int]] = None, reps: int = 20,
                     device="cuda", return_times: bool = False):
@@ -40,7 +58,6 @@ def suggest_x_alloc(extents: Sequence[int], halo: int, dtype=None,
     return_times: also return {x_alloc: microseconds per step}."""
     import torch
 
-    import ghex_amd
     from ghex_amd import _ghx
     from ghex_amd.structured import regular as R
     dtype = torch.float64 if dtype is None else dtype
@@ -55,7 +72,7 @@ def suggest_x_alloc(extents: Sequence[int], halo: int, dtype=None,
         base = -(-ex // step) * step  # smallest 16-B aligned width >= ex
         candidates = [base + k * step for k in range(0, max(1, 16 // step) + 1)]
         candidates = sorted({ex, *candidates})
-    ctx = ghex_amd.make_context()
+    ctx = _LocalContext()  # this process alone, even under torch.distributed (no collective)
     dd = R.DomainDescriptor(0, first, last)
     pc = R.make_pattern(ctx, R.HaloGenerator(first, last, (h,) * 6, (True,) * 3), [dd])
     L = _ghx.lib()
