@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--no-cold", action="store_true",
                    help="skip the cold-cache launch times (their extra launches of the same "
                         "kernels would skew a profiler's per-kernel averages)")
+    p.add_argument("--no-layout", action="store_true",
+                   help="skip the padded-layout leg (its launches share the headline kernel's "
+                        "grid and would mix into a profiler's per-kernel averages)")
     p.add_argument("--bulk", action="store_true",
                    help="N>1: also time the zero-copy bulk exchange (IPC puts into peer halos); "
                         "always on at N=1 (self puts)")
@@ -559,7 +562,7 @@ def extras(args, torch, dist, dev, stream, out, v):
     # the north star's other halo widths, same decomposition, same two-launch step, verified
     out["halo_widths"] = {str(h): bench_halo(h, v, torch, dist, dev, stream, args)
                           for h in (1, 3) if h != Hw}
-    if world == 1 and N == 512 and Hw == 2:
+    if world == 1 and N == 512 and Hw == 2 and not args.no_layout:
         # the same cells and bytes in a field whose x rows are allocated 2 cells wider (row pitch
         # 4,144 B instead of 4,128 B): what the x-face lines' address set costs
         out["layout_x_alloc_518"] = bench_halo(Hw, v, torch, dist, dev, stream, args, x_alloc=518)

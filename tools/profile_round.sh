@@ -11,8 +11,9 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 if [ "${PMC_ONLY:-0}" != 1 ]; then
 # 1) the bench command itself (defaults: N=1, 512^3, H=2, hipGraph, extras, cpu baseline) minus
-#    the cold-cache legs, whose extra launches of the same kernels would skew the averages
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/bench -o kt --output-format csv -- python3 $R/bench.py --no-cold > $OUT/bench.log 2>&1
+#    the cold-cache legs and the padded-layout leg, whose extra launches of the same kernels
+#    (same grids) would skew the per-kernel averages
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/bench -o kt --output-format csv -- python3 $R/bench.py --no-cold --no-layout > $OUT/bench.log 2>&1
 # 2) kernel traces at halo 1 and 3
 for h in 1 3; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/h$h -o kt --output-format csv -- python3 $R/bench.py --halo $h --no-extras --no-cpu-baseline --no-cold > $OUT/h$h.log 2>&1
