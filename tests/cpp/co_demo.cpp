@@ -11,6 +11,9 @@
 //   co_demo bulkloop PX PY PZ N H       the same two fields through the C++
 //                                        bulk_communication_object (zero-copy puts between the
 //                                        thread-ranks' fields, no buffers)
+//   co_demo rma NRANKS                  test_local_rma.cpp's geometry (two domains per rank,
+//                                        offset 3 > halo 2, double/float/int fields) through the
+//                                        C++ bulk_communication_object
 //   co_demo rccl N H SELF [PIPE]         one rank, RCCL communicator on device 0; SELF=1 sends the
 //                                        self messages through ncclSend/ncclRecv (group), SELF=0
 //                                        takes the fused self path; PIPE=1 the pipelined form
@@ -256,6 +259,134 @@ int unstructured_case(const char* file, int levels)
     return (bad == 0 && errors == 0) ? 0 : 1;
 }
 
+// test/structured/regular/test_local_rma.cpp's simulation_1 geometry through the C++ bulk object:
+// n ranks as threads, TWO domains per rank (ids 2r, 2r+1, local extent 4x3x2), fields allocated
+// with offset 3 > halo 2 (extent 10x9x8), three value types per domain (double, float, int), one
+// bulk object per rank with all six fields. Owned cell = wrapped global linear index + type
+// number; after two exchanges every cell within the halo equals its wrapped value and every cell
+// beyond it is untouched (-1).
+template<typename T>
+long rma_check(const std::vector<T>& h, const std::array<int, 3>& first, const std::array<int, 3>& G,
+               int k)
+{
+    long bad = 0;
+    for (int z = 0; z < 8; ++z)
+        for (int y = 0; y < 9; ++y)
+            for (int x = 0; x < 10; ++x)
+            {
+                const int l[3] = {x - 3, y - 3, z - 3};
+                const int ext[3] = {4, 3, 2};
+                bool in_halo = true;
+                for (int d = 0; d < 3; ++d) in_halo = in_halo && l[d] >= -2 && l[d] < ext[d] + 2;
+                long g[3];
+                for (int d = 0; d < 3; ++d) g[d] = ((first[std::size_t(d)] + l[d]) % G[std::size_t(d)] + G[std::size_t(d)]) % G[std::size_t(d)];
+                const T want = in_halo ? T(g[0] + long(G[0]) * (g[1] + long(G[1]) * g[2]) + k) : T(-1);
+                bad += h[std::size_t((z * 9 + y) * 10 + x)] != want;
+            }
+    return bad;
+}
+
+int rma_case(int n)
+{
+    loopback_hub hub(n);
+    std::vector<loopback_transport> ts;
+    for (int r = 0; r < n; ++r) ts.emplace_back(hub, r);
+    std::atomic<long> bad{0};
+    std::atomic<int> errors{0};
+    const std::array<int, 3> G{16, ((n - 1) / 2 + 1) * 3, 2};
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; ++r)
+        th.emplace_back([&, r] {
+            try
+            {
+                check_hip(hipSetDevice(0), "hipSetDevice");
+                context ctx(ts[std::size_t(r)]);
+                std::vector<R::domain_descriptor> doms;
+                for (int k = 0; k < 2; ++k)
+                    doms.emplace_back(2 * r + k,
+                                      std::array<int, 3>{((r % 2) * 2 + k) * 4, (r / 2) * 3, 0},
+                                      std::array<int, 3>{((r % 2) * 2 + k + 1) * 4 - 1, (r / 2 + 1) * 3 - 1, 1});
+                R::halo_generator hg{{0, 0, 0}, {G[0] - 1, G[1] - 1, G[2] - 1}, {2, 2, 2, 2, 2, 2},
+                                     {true, true, true}};
+                auto pattern = R::make_pattern(ctx, hg, doms);
+                const std::size_t cells = 10 * 9 * 8;
+                std::vector<double*> dd(2);
+                std::vector<float*> df(2);
+                std::vector<int*> di(2);
+                auto fill = [&](auto* dev, int dom, int k) {
+                    using T = std::remove_pointer_t<decltype(dev)>;
+                    std::vector<T> h(cells, T(-1));
+                    const auto& f = doms[std::size_t(dom)].first();
+                    for (int z = 0; z < 2; ++z)
+                        for (int y = 0; y < 3; ++y)
+                            for (int x = 0; x < 4; ++x)
+                                h[std::size_t(((z + 3) * 9 + y + 3) * 10 + x + 3)] =
+                                    T(f[0] + x + long(G[0]) * (f[1] + y + long(G[1]) * (f[2] + z)) + k);
+                    check_hip(hipMemcpy(dev, h.data(), cells * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+                };
+                std::vector<std::unique_ptr<structured::field_descriptor<double, 3>>> fd;
+                std::vector<std::unique_ptr<structured::field_descriptor<float, 3>>> ff;
+                std::vector<std::unique_ptr<structured::field_descriptor<int, 3>>> fi;
+                bulk_communication_object bco(ctx);
+                for (int k = 0; k < 2; ++k)
+                {
+                    check_hip(hipMalloc(&dd[std::size_t(k)], cells * 8), "hipMalloc");
+                    check_hip(hipMalloc(&df[std::size_t(k)], cells * 4), "hipMalloc");
+                    check_hip(hipMalloc(&di[std::size_t(k)], cells * 4), "hipMalloc");
+                    const int id = 2 * r + k;
+                    fd.emplace_back(new structured::field_descriptor<double, 3>(id, dd[std::size_t(k)], {3, 3, 3}, {10, 9, 8}, {2, 1, 0}));
+                    ff.emplace_back(new structured::field_descriptor<float, 3>(id, df[std::size_t(k)], {3, 3, 3}, {10, 9, 8}, {2, 1, 0}));
+                    fi.emplace_back(new structured::field_descriptor<int, 3>(id, di[std::size_t(k)], {3, 3, 3}, {10, 9, 8}, {2, 1, 0}));
+                }
+                // registration order as the reference test: 1a 1b 2a 2b 3a 3b
+                bco.add_field(pattern(*fd[0]));
+                bco.add_field(pattern(*fd[1]));
+                bco.add_field(pattern(*ff[0]));
+                bco.add_field(pattern(*ff[1]));
+                bco.add_field(pattern(*fi[0]));
+                bco.add_field(pattern(*fi[1]));
+                bco.init();
+                long b = 0;
+                for (int rep = 0; rep < 2; ++rep)
+                {
+                    for (int k = 0; k < 2; ++k)
+                    {
+                        fill(dd[std::size_t(k)], k, 0);
+                        fill(df[std::size_t(k)], k, 1);
+                        fill(di[std::size_t(k)], k, 2);
+                    }
+                    bco.exchange().wait();
+                    for (int k = 0; k < 2; ++k)
+                    {
+                        std::vector<double> hd(cells);
+                        std::vector<float> hf(cells);
+                        std::vector<int> hi(cells);
+                        check_hip(hipMemcpy(hd.data(), dd[std::size_t(k)], cells * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+                        check_hip(hipMemcpy(hf.data(), df[std::size_t(k)], cells * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+                        check_hip(hipMemcpy(hi.data(), di[std::size_t(k)], cells * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+                        const auto& f = doms[std::size_t(k)].first();
+                        b += rma_check(hd, f, G, 0) + rma_check(hf, f, G, 1) + rma_check(hi, f, G, 2);
+                    }
+                }
+                std::printf("{\"mode\":\"rma\",\"rank\":%d,\"puts\":%zu,\"bad\":%ld}\n", r, bco.num_puts(), b);
+                bad += b;
+                for (int k = 0; k < 2; ++k)
+                {
+                    (void)hipFree(dd[std::size_t(k)]);
+                    (void)hipFree(df[std::size_t(k)]);
+                    (void)hipFree(di[std::size_t(k)]);
+                }
+            }
+            catch (const std::exception& e)
+            {
+                std::printf("{\"rank\":%d,\"error\":\"%s\"}\n", r, e.what());
+                ++errors;
+            }
+        });
+    for (auto& t : th) t.join();
+    return (bad == 0 && errors == 0) ? 0 : 1;
+}
+
 int bench(int N, int H, int iters)
 {
     check_hip(hipSetDevice(0), "hipSetDevice");
@@ -298,6 +429,7 @@ int main(int argc, char** argv)
         if (mode == "bulkloop" && argc == 7)
             return loopback(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
                             std::atoi(argv[6]), false, true);
+        if (mode == "rma" && argc == 3) return rma_case(std::atoi(argv[2]));
         if (mode == "rccl" && argc == 5) return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
         if (mode == "rccl" && argc == 6)
             return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]));

@@ -167,3 +167,15 @@ def test_bulk_header_compiles_host_only(tmp_path):
                     "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{LIB}",
                     "-Wl,-rpath,/opt/rocm/lib"], check=True)
     assert subprocess.run([str(exe)]).returncode == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4])
+def test_co_bulk_reference_local_rma_geometry(n):
+    """test/structured/regular/test_local_rma.cpp's simulation_1 through the C++ bulk object:
+    two domains per rank (self puts between them), fields with offset 3 > halo 2, double /
+    float / int fields registered in the reference's order; halos filled, beyond untouched."""
+    rc, lines, err = _run(["rma", n])
+    ranks = [l for l in lines if l.get("mode") == "rma"]
+    assert rc == 0, (lines, err)
+    assert len(ranks) == n and all(l["bad"] == 0 and l["puts"] >= 1 for l in ranks)
