@@ -462,6 +462,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 3) throw invalid("nt must be 0, 1, 2 or 3");
             g_tune.nt = value;
         }
+        else if (k == "nt_dir")
+        {
+            if (value < 0 || value > 2) throw invalid("nt_dir must be 0, 1 or 2");
+            g_tune.nt_dir = value;
+        }
         else if (k == "order")
         {
             if (value < 0 || value > 4) throw invalid("order must be in 0..4");

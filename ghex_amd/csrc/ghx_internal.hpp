@@ -28,6 +28,7 @@ struct tuning
 {
     int unroll = 4;                 // vectors in flight per lane per loop trip: 2, 4, 8
     int nt = 0;                     // 0 default, 1 nt stores, 2 nt loads + stores, 3 nt loads
+    int nt_dir = 0;                 // nt applies to: 0 both directions, 1 pack, 2 unpack
     int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
     uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
     uint32_t self_tile_bytes = kTileBytes;  // the same for the fused self exchange (separate

@@ -1008,7 +1008,9 @@ __global__ __launch_bounds__(kBlock) void k_put(kargs a)
 template<typename Seg, bool PACK, int U>
 void launch_nt(const kargs& a, hipStream_t s, uint32_t grid)
 {
-    switch (g_tune.nt)
+    // nt_dir: 0 the policy applies to both directions, 1 to the pack only, 2 to the unpack only
+    const int nt = (g_tune.nt_dir == 0 || (g_tune.nt_dir == 1) == PACK) ? g_tune.nt : 0;
+    switch (nt)
     {
         case 1: launch((k_copy<PACK, U, 1, Seg>), grid, s, a); break;
         case 2: launch((k_copy<PACK, U, 2, Seg>), grid, s, a); break;

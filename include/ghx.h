@@ -45,7 +45,8 @@ typedef void* ghx_stream;
 
 /* Process-wide tuning knobs (development / benchmarking; defaults are the measured best):
  * "unroll" (2|4|8 vectors in flight per lane), "nt" (0 default cache policy, 1 non-temporal
- * stores, 2 non-temporal loads and stores), "grid_cap" (max workgroups, 0 = one per tile),
+ * stores, 2 non-temporal loads and stores, 3 non-temporal loads), "nt_dir" (0|1|2: "nt" applies
+ * to both directions, the pack only, the unpack only), "grid_cap" (max workgroups, 0 = one per tile),
  * "tile_bytes" (buffer bytes per workgroup tile), "small_tile_rows", "small_row_bytes",
  * "u_tile_rows" (rows per tile of short-row index-list segments), "usort" (0|1: visit index
  * lists in ascending field order),

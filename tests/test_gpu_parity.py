@@ -414,7 +414,8 @@ def test_full_size_512_h2_checksum():
                                    {"short_xcds": 3, "small_tile_rows": 64},
                                    {"lds": 1}, {"lds": 1, "small_tile_rows": 100},
                                    {"xcd_rotate": 1, "small_tile_rows": 64},
-                                   {"xcd_rotate": 2, "small_tile_rows": 64}],
+                                   {"xcd_rotate": 2, "small_tile_rows": 64},
+                                   {"nt": 3, "nt_dir": 2}, {"nt": 1, "nt_dir": 1}],
                          ids=lambda d: "-".join(f"{k}={v}" for k, v in d.items()))
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_tuning_variants_stay_bit_exact(knobs, Hw):
