@@ -76,7 +76,62 @@ def parse():
     p.add_argument("--extras-timeout", type=float, default=240.0,
                    help="seconds the extras (after the headline) may take before the line is "
                         "printed without them")
+    p.add_argument("--init-timeout", type=float, default=300.0,
+                   help="seconds init_process_group + the setup all-gather may take; on expiry "
+                        "the line is printed with verified=false and an error, exit 3")
+    p.add_argument("--exchange-timeout", type=float, default=300.0,
+                   help="seconds the verified full exchange (the first RCCL traffic) may take; "
+                        "on expiry as --init-timeout")
+    p.add_argument("--headline-timeout", type=float, default=600.0,
+                   help="seconds the headline measurement (graphs, warmup, timed region, "
+                        "kernel durations) may take; on expiry as --init-timeout")
     return p.parse_args()
+
+
+class StageGuard:
+    """Bounds the stages before the headline line can be printed (init_process_group, the first
+    cross-GPU exchange, the timed region). If a stage does not finish in time — a peer died or
+    the transport hangs, which a rank blocked inside RCCL can neither see nor leave — rank 0
+    prints the line with value null, verified false and an `error` naming the stage, and every
+    rank exits with status 3 (os._exit from the guard thread: the stuck thread cannot be joined,
+    and nothing is re-executed or retried). Other ranks report to stderr only."""
+
+    EXIT_CODE = 3
+
+    def __init__(self, line, rank=0):
+        self.line = line  # the JSON fields known so far (metric, n_gpus, config ...)
+        self.rank = rank
+
+    def expire(self, name, seconds):
+        o = dict(self.line)
+        o.update(value=None, verified=False, stage=name,
+                 error=f"stage '{name}' did not complete within {seconds:.0f} s on rank "
+                       f"{self.rank} (a peer or the transport hung); no measurement")
+        msg = json.dumps(o)
+        if self.rank == 0:
+            print(msg, flush=True)
+        else:
+            print(msg, file=sys.stderr, flush=True)
+        sys.stderr.flush()
+        os._exit(self.EXIT_CODE)
+
+    def stage(self, name, seconds):
+        import contextlib
+        import threading
+
+        @contextlib.contextmanager
+        def guarded():
+            done = threading.Event()
+
+            def watch():
+                if not done.wait(seconds):
+                    self.expire(name, seconds)
+            threading.Thread(target=watch, daemon=True, name=f"guard:{name}").start()
+            try:
+                yield
+            finally:
+                done.set()
+        return guarded()
 
 
 def spawn_workers(args) -> int:
@@ -181,16 +236,32 @@ def main():
         raise SystemExit(f"--gpus must be one of {sorted(DECOMP)}")
     if args.rehearse:
         local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     distributed = world > 1 or args.force_dist
     backend = None
-    if distributed:
-        backend = "gloo" if args.rehearse else "nccl"
-        if args.rehearse:
-            dist.init_process_group("gloo")
+    N, Hw = args.N, args.halo
+    parts = DECOMP[world]
+    guard = StageGuard({
+        "metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "config": {"N": N, "halo": Hw, "decomposition": list(parts)}}, rank)
+    with guard.stage("init_process_group", args.init_timeout):
+        if distributed:
+            import datetime
+            backend = "gloo" if args.rehearse else "nccl"
+            # the process group's own timeout stays above the guard's stages, so a stuck
+            # collective is reported by the guard (with a line), not aborted by the watchdog
+            pg_timeout = datetime.timedelta(seconds=60 + max(
+                args.init_timeout, args.exchange_timeout, args.headline_timeout))
+            if args.rehearse:
+                dist.init_process_group("gloo", timeout=pg_timeout)
+                torch.cuda.set_device(local)
+            else:
+                torch.cuda.set_device(local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                        timeout=pg_timeout)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
 
     def barrier():
         if args.rehearse:
@@ -212,9 +283,7 @@ def main():
         k, v = kv.split("=")
         _ghx.call("ghx_tune", k.encode(), int(v))
 
-    N, Hw = args.N, args.halo
     E = N + 2 * Hw
-    parts = DECOMP[world]
     G = [parts[d] * N for d in range(3)]
     c = (rank % parts[0], (rank // parts[0]) % parts[1], rank // (parts[0] * parts[1]))
     first = tuple(c[d] * N for d in range(3))
@@ -223,7 +292,8 @@ def main():
     ctx = ghex_amd.make_context()
     dd = R.DomainDescriptor(rank, first, last)
     hg = R.HaloGenerator((0, 0, 0), tuple(g - 1 for g in G), (Hw,) * 6, (True,) * 3)
-    pc = R.make_pattern(ctx, hg, [dd])
+    with guard.stage("pattern_setup", args.init_timeout):  # the setup all-gather
+        pc = R.make_pattern(ctx, hg, [dd])
 
     # synthetic field: owned cell = global linear index (exact in fp64), halo = -1
     base = torch.full((E, E, E), -1.0, dtype=torch.float64, device=dev)
@@ -254,8 +324,11 @@ def main():
             ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)))
 
     # ---- verified full exchange (pack -> RCCL -> unpack) --------------------------------------
-    co.exchange(bis).wait()
-    verified = verify() == 0
+    with guard.stage("verified_exchange", args.exchange_timeout):
+        co.exchange(bis).wait()
+        verified = verify() == 0
+    headline = guard.stage("headline", args.headline_timeout)
+    headline.__enter__()
 
     plan = co.plan(bis)
     send, recv = co.buffers(plan, dev)
@@ -407,6 +480,8 @@ def main():
         "step_frac": round(step_bytes / dev_step / 1e9 / HBM_PEAK_GBS, 4),
     }
 
+    headline.__exit__(None, None, None)
+
     # ---- extras (bounded: the line is printed without them if they overrun) -------------------
     done = threading.Event()
     printed = threading.Lock()
@@ -537,21 +612,27 @@ def extras(args, torch, dist, dev, stream, out, v):
             out["transport_error"] = f"{type(e).__name__}: {str(e)[:200]}"
         co.exchange(bis).wait()  # halos valid again (the recv buffers were overwritten)
     if world > 1:
-        # per-peer streams (rehearsal: the host-staged form of the same pipeline over gloo)
-        cop = R.make_communication_object(v["ctx"], pipelined=True,
-                                          staging="host" if args.rehearse else None)
-        v["clear_halos"]()
-        cop.exchange(bis).wait()
-        okp = v["verify"]() == 0
-        for _ in range(3):
+        # per-peer streams (rehearsal: the host-staged form of the same pipeline over gloo); the
+        # pair communicators are created here, at the first pipelined exchange: their failure is
+        # reported in this leg and never reaches the headline
+        try:
+            cop = R.make_communication_object(v["ctx"], pipelined=True,
+                                              staging="host" if args.rehearse else None)
+            v["clear_halos"]()
             cop.exchange(bis).wait()
-        Tp = timed(lambda: cop.exchange(bis).wait(), ke)
-        out["exchange_pipelined"] = {"ms_per_step": round(Tp / ke * 1e3, 4), "verified": okp,
-                                     "mode": "per-peer streams: pack, " +
-                                             ("D2H, gloo send/recv, H2D" if args.rehearse else
-                                              "one RCCL group on the pair's own communicator") +
-                                             " and unpack of each peer's buffers on its stream"}
-        del cop
+            okp = v["verify"]() == 0
+            for _ in range(3):
+                cop.exchange(bis).wait()
+            Tp = timed(lambda: cop.exchange(bis).wait(), ke)
+            out["exchange_pipelined"] = {"ms_per_step": round(Tp / ke * 1e3, 4), "verified": okp,
+                                         "mode": "per-peer streams: pack, " +
+                                                 ("D2H, gloo send/recv, H2D" if args.rehearse else
+                                                  "one RCCL group on the pair's own communicator") +
+                                                 " and unpack of each peer's buffers on its stream"}
+            del cop
+        except Exception as e:  # reported; the legs after it still run
+            out["exchange_pipelined"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+        co.exchange(bis).wait()  # halos valid again
     if world > 1:
         # the unstructured path between real ranks (BASELINE config 5's shape, scaled to 1M cells
         # per rank so the setup all-gather stays small): verified and timed
@@ -1024,37 +1105,80 @@ def bench_config5(torch, dev, _ghx, levels):
             "index_bytes_per_exchange": 2 * nh * 4}
 
 
+def _cpu_info():
+    """CPU model (/proc/cpuinfo), nproc, and the cores this process may run on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        share = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        share = list(range(os.cpu_count() or 1))
+    return model, os.cpu_count(), share
+
+
+def _pin(core):
+    """Pin the CALLING thread to one core (Linux: sched_setaffinity with pid 0 applies to the
+    calling thread), the in-process form of BASELINE.md's `taskset -c <core>`."""
+    try:
+        os.sched_setaffinity(0, {core})
+        return True
+    except (AttributeError, OSError):
+        return False
+
+
 def cpu_baseline(N, Hw, seconds):
     """The oracle's single-thread C restatement of serialization<cpu>::pack_batch/unpack_batch
-    (include/ghex/structured/pack_kernels.hpp:62-158) on the same workload, bounded in time."""
+    (include/ghex/structured/pack_kernels.hpp:62-158) on the same workload, bounded in time,
+    run in a thread pinned to one core (the first core of this process's affinity set)."""
+    import threading
+
     import numpy as np
     from oracle import oracle as orc
+    model, nproc, share = _cpu_info()
     E = N + 2 * Hw
-    a = np.zeros((E, E, E))
-    a[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = np.arange(N ** 3, dtype=np.float64).reshape(N, N, N)
     dom = orc.RegularDomain(0, (0, 0, 0), (N - 1,) * 3)
     pat = orc.regular_make_pattern([[dom]], (0, 0, 0), (N - 1,) * 3, (Hw,) * 6, (1, 1, 1))[0][0]
-    spec = orc.FieldSpec(a, 8, (2, 1, 0), (Hw,) * 3, (E,) * 3)
     send = list(pat.send.values())[0][1]
     recv = list(pat.recv.values())[0][1]
     nbytes = sum(b.size() for b in send) * 8
-    buf = np.zeros(nbytes, np.uint8)
-    orc.structured_pack(spec, buf, send)
-    orc.structured_unpack(spec, buf, recv)
-    t0 = time.perf_counter()
-    it = 0
-    while True:
+    res = {}
+
+    def one():
+        res["pinned"] = _pin(share[0])
+        a = np.zeros((E, E, E))
+        a[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = np.arange(N ** 3, dtype=np.float64).reshape(N, N, N)
+        spec = orc.FieldSpec(a, 8, (2, 1, 0), (Hw,) * 3, (E,) * 3)
+        buf = np.zeros(nbytes, np.uint8)
         orc.structured_pack(spec, buf, send)
         orc.structured_unpack(spec, buf, recv)
-        it += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds and it >= 3:
-            break
+        t0 = time.perf_counter()
+        it = 0
+        while True:
+            orc.structured_pack(spec, buf, send)
+            orc.structured_unpack(spec, buf, recv)
+            it += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds and it >= 3:
+                break
+        res["it"], res["dt"] = it, dt
+    th = threading.Thread(target=one)
+    th.start()
+    th.join()
+    it, dt = res["it"], res["dt"]
     gbs = 4 * nbytes * it / dt / 1e9
     out = {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+           "cpu_model": model, "nproc": nproc, "affinity_cores": len(share),
+           "pinned_core": share[0] if res["pinned"] else None,
            "sample": f"{N}^3 fp64 H={Hw} one periodic domain, pack+unpack x{it} "
-                     f"({dt:.1f} s, 1 thread, oracle/ghex_oracle.c row-memcpy restatement)"}
-    del a, buf
+                     f"({dt:.1f} s, 1 thread pinned to core {share[0]}, "
+                     f"oracle/ghex_oracle.c row-memcpy restatement)"}
     out["ranks"] = cpu_baseline_ranks(N, Hw, seconds, orc, nbytes, send, recv)
     return out
 
@@ -1062,21 +1186,21 @@ def cpu_baseline(N, Hw, seconds):
 def cpu_baseline_ranks(N, Hw, seconds, orc, nbytes, send, recv):
     """the same single-threaded serializer run as independent ranks, one per host
     core of the box's CPU share (each rank its own 512^3 domain and buffer, like the reference's
-    one-rank-per-core CPU runs). The C oracle releases the GIL inside its ctypes calls, so the
-    ranks are threads of this process; value = bytes summed over ranks / the slowest rank's time."""
+    one-rank-per-core CPU runs), each pinned to its own core. The C oracle releases the GIL
+    inside its ctypes calls, so the ranks are threads of this process (no re-exec from a process
+    that has touched the GPU); value = bytes summed over ranks / the slowest rank's time."""
     import threading
 
     import numpy as np
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count() or 1
-    ranks = max(1, min(16, share))  # the GPU box grants 16 cores per GPU (its nproc shows more)
+    model, nproc, share = _cpu_info()
+    ranks = max(1, min(16, len(share)))  # the GPU box grants 16 cores per GPU (nproc shows more)
     E = N + 2 * Hw
     res = [None] * ranks
+    pinned = [False] * ranks
     barrier = threading.Barrier(ranks)
 
     def rank_fn(r):
+        pinned[r] = _pin(share[r])
         a = np.zeros((E, E, E))
         a[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = r
         spec = orc.FieldSpec(a, 8, (2, 1, 0), (Hw,) * 3, (E,) * 3)
@@ -1104,9 +1228,11 @@ def cpu_baseline_ranks(N, Hw, seconds, orc, nbytes, send, recv):
     slowest = max(dt for _, dt in res)
     its = [it for it, _ in res]
     return {"value": round(total / slowest / 1e9, 3), "unit": "GB/s", "cores": ranks,
-            "kind": "port",
-            "sample": f"{ranks} independent ranks, each a {N}^3 fp64 H={Hw} periodic domain, "
-                      f"pack+unpack x{min(its)}-{max(its)} in {slowest:.1f} s, one thread each "
+            "kind": "port", "cpu_model": model, "nproc": nproc, "affinity_cores": len(share),
+            "pinned": all(pinned),
+            "sample": f"{ranks} independent ranks, each a {N}^3 fp64 H={Hw} periodic domain "
+                      f"pinned to its own core ({share[0]}..{share[ranks - 1]}), pack+unpack "
+                      f"x{min(its)}-{max(its)} in {slowest:.1f} s, one thread each "
                       f"(oracle/ghex_oracle.c)"}
 
 

@@ -176,6 +176,10 @@ class CommunicationObject:
                  rccl_self: bool = False, max_streams: int = 4):
         if staging not in (None, "host"):
             raise ValueError("staging must be None (device buffers) or 'host'")
+        if rccl_self and staging == "host":
+            # the host-staged pipeline keeps self messages on the device (recv aliases send);
+            # routing them through RCCL is a device-buffer-only test mode
+            raise ValueError("rccl_self applies to device buffers only (staging=None)")
         self.context = context
         self.fuse_self = fuse_self
         self.staging = staging
@@ -186,7 +190,6 @@ class CommunicationObject:
         # pipelined: peers dealt over this many streams in round order (hardware queues are few)
         self.max_streams = max(1, int(max_streams))
         self._streams = {}
-        self._comms = {}
         self._plans = {}
         self._bufs = {}
         self._host = {}
@@ -347,7 +350,15 @@ class CommunicationObject:
                                   _ghx.ptr_array([t.data_ptr() for t in send]),
                                   _ghx.ptr_array([t.data_ptr() for t in recv]))
         fptrs, sptrs, rptrs = arrs
+        # an exchange is "in flight" (exchange() again before wait() raises) only once it has
+        # been enqueued: a failure while posting it leaves the object usable
+        h = self._enqueue(bis, plan, send, recv, fptrs, sptrs, rptrs, stream)
         self._valid = True
+        return h
+
+    def _enqueue(self, bis, plan, send, recv, fptrs, sptrs, rptrs, stream):
+        import torch
+        device = bis[0].field.device
         if self.pipelined:
             if self.staging == "host":
                 self._exchange_host_pipelined(plan, send, recv, fptrs, sptrs, rptrs, len(bis),
@@ -439,34 +450,10 @@ class CommunicationObject:
             plan._split = True
 
     def _rccl_comms(self, peers):
-        """One 2-rank RCCL communicator per peer pair (setup time, collective over the context:
-        every rank reaches its first pipelined exchange of a plan together). The lower rank of a
-        pair draws the unique id; ids travel by the setup all-gather; communicators are created
-        in round order (each ncclCommInitRank blocks until both ends have called it)."""
-        import os
-        import torch
+        """The context's pair communicators (Context.pair_communicators), created in round
+        order at the first pipelined exchange that needs them, reused afterwards."""
         me, world = self.context.rank(), self.context.size()
-        _ghx.call("ghx_rccl_open", os.path.join(os.path.dirname(torch.__file__), "lib",
-                                                "librccl.so").encode())
-        want = [p for p in peers if p not in self._comms]
-        mine = {}
-        for p in want:
-            if p == me or me < p:
-                buf = (ctypes.c_ubyte * 128)()
-                _ghx.call("ghx_rccl_unique_id", buf)
-                mine[(me, p)] = bytes(buf)
-        every = self.context.all_gather_object(mine)
-        for p in peer_order(me, want, world):
-            a, b = min(me, p), max(me, p)
-            uid = every[a].get((a, b))  # drawn by the lower rank of the pair
-            if uid is None:
-                raise RuntimeError(f"no RCCL id for pair {(a, b)}: ranks disagree on peers")
-            comm = ctypes.c_void_p()
-            n = 1 if p == me else 2
-            _ghx.call("ghx_rccl_comm_init", (ctypes.c_ubyte * 128).from_buffer_copy(uid), n,
-                      0 if me <= p else 1, ctypes.byref(comm))
-            self._comms[p] = (comm, 0 if p == me else (1 if me < p else 0))
-        return [self._comms[p] for p in peers]
+        return self.context.pair_communicators(peers, lambda ps: peer_order(me, ps, world))
 
     def _pipeline_of(self, plan, device):
         pl = getattr(plan, "_pipeline", None)

@@ -2,6 +2,8 @@
 Python: bindings/python/src/ghex/context.py make_context)."""
 from __future__ import annotations
 
+import ctypes
+
 
 class Context:
     """Wraps a torch.distributed process group (or a single process when none is initialised).
@@ -18,6 +20,9 @@ class Context:
             self._size = self._dist.get_world_size(group)
         else:
             self._rank, self._size = 0, 1
+        # pipelined exchanges: one 2-rank RCCL communicator per peer pair, created on first use
+        # and shared by every communication object of this context (destroyed with it)
+        self._pair_comms = {}
 
     def rank(self) -> int:
         return self._rank
@@ -37,6 +42,56 @@ class Context:
         out = [None] * self._size
         self._dist.all_gather_object(out, obj, group=self.group)
         return out
+
+    def pair_communicators(self, peers, order):
+        """One 2-rank RCCL communicator per peer (a 1-rank one for this rank itself), created at
+        the first request (setup time, collective over the context: every rank reaches it
+        together) and reused by every later pipelined exchange of this context. The lower rank of
+        a pair draws the unique id; ids travel by the setup all-gather; communicators are
+        created in `order` (the global round order: each ncclCommInitRank blocks until both ends
+        have called it). Returns [(comm handle, this rank's rank in it)] in `peers` order."""
+        import os
+
+        import torch
+
+        from . import _ghx
+        me = self.rank()
+        want = [p for p in peers if p not in self._pair_comms]
+        if want:
+            _ghx.call("ghx_rccl_open", os.path.join(os.path.dirname(torch.__file__), "lib",
+                                                    "librccl.so").encode())
+        mine = {}
+        for p in want:
+            if p == me or me < p:
+                buf = (ctypes.c_ubyte * 128)()
+                _ghx.call("ghx_rccl_unique_id", buf)
+                mine[(me, p)] = bytes(buf)
+        every = self.all_gather_object(mine) if want else []
+        for p in order(want):
+            a, b = min(me, p), max(me, p)
+            uid = every[a].get((a, b))  # drawn by the lower rank of the pair
+            if uid is None:
+                raise RuntimeError(f"no RCCL id for pair {(a, b)}: ranks disagree on peers")
+            comm = ctypes.c_void_p()
+            n = 1 if p == me else 2
+            _ghx.call("ghx_rccl_comm_init", (ctypes.c_ubyte * 128).from_buffer_copy(uid), n,
+                      0 if me <= p else 1, ctypes.byref(comm))
+            self._pair_comms[p] = (comm, 0 if p == me else (1 if me < p else 0))
+        return [self._pair_comms[p] for p in peers]
+
+    def close(self):
+        """Destroy the pair communicators (every pipeline that uses them must be gone)."""
+        comms, self._pair_comms = self.__dict__.get("_pair_comms", {}), {}
+        if comms:
+            from . import _ghx
+            for comm, _ in comms.values():
+                _ghx.lib().ghx_rccl_comm_destroy(comm)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def global_rank(self, group_rank: int) -> int:
         if self._dist is None or self.group is None:

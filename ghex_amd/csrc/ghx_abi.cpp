@@ -31,19 +31,30 @@ namespace
 // the content (descriptor, iteration spaces, direction); the unstructured entry keeps a host
 // copy of its index list and compares it in full on every hit, so a list mutated in place gets
 // a fresh plan. Evicted or replaced plans are never freed under the lock with a device-wide
-// synchronisation: they are retired and freed once the event recorded after their last
-// execution has completed (plans executed inside a stream capture are kept: a graph may still
-// reference their device tables).
+// synchronisation: they are retired and freed once every stream that executed them has passed
+// the event recorded after its last execution there (plans executed inside a stream capture are
+// kept: a graph may still reference their device tables).
 template<typename Plan>
 struct cached_plan
 {
+    struct use
+    {
+        hipStream_t stream;
+        hipEvent_t done;  // recorded after the latest execution on `stream`
+    };
     std::unique_ptr<Plan> plan;
     std::vector<char> content;  // unstructured: the index list bytes the plan was built from
-    hipEvent_t last = nullptr;  // recorded after each execution on a non-capturing stream
+    std::vector<use> uses;      // one record per stream that has executed the plan
     bool captured = false;
+    bool idle() const
+    {
+        for (const auto& u : uses)
+            if (hipEventQuery(u.done) != hipSuccess) return false;
+        return true;
+    }
     ~cached_plan()
     {
-        if (last) (void)hipEventDestroy(last);
+        for (auto& u : uses) (void)hipEventDestroy(u.done);
     }
 };
 
@@ -63,8 +74,7 @@ class plan_lru
         std::vector<entry> keep;
         for (auto& e : retired_)
         {
-            const bool idle = e.use_count() == 1 && !e->captured &&
-                              (!e->last || hipEventQuery(e->last) == hipSuccess);
+            const bool idle = e.use_count() == 1 && !e->captured && e->idle();
             if (!idle) keep.push_back(std::move(e));
         }
         retired_.swap(keep);
@@ -106,7 +116,10 @@ class plan_lru
         return fresh;
     }
 
-    // stream-ordered record of a use (no host synchronisation)
+    // stream-ordered record of a use (no host synchronisation). One event per stream: a later
+    // execution on the same stream is ordered after the earlier ones, so re-recording that
+    // stream's event keeps covering them; an execution on another stream gets its own record,
+    // so a plan used on streams A then B is freed only once BOTH have passed their last use.
     void used(cached_plan<Plan>& c, void* stream)
     {
         hipStream_t s = static_cast<hipStream_t>(stream);
@@ -118,13 +131,34 @@ class plan_lru
             c.captured = true;
             return;
         }
-        if (!c.last && hipEventCreateWithFlags(&c.last, hipEventDisableTiming) != hipSuccess)
+        for (auto& u : c.uses)
+            if (u.stream == s)
+            {
+                if (hipEventRecord(u.done, s) != hipSuccess) c.captured = true;
+                return;
+            }
+        // a new stream: drop the records of streams that have passed their last use (bounds
+        // the list for callers that rotate through many streams)
+        std::vector<typename cached_plan<Plan>::use> live;
+        for (auto& u : c.uses)
         {
-            c.last = nullptr;
+            if (hipEventQuery(u.done) == hipSuccess) (void)hipEventDestroy(u.done);
+            else live.push_back(u);
+        }
+        c.uses.swap(live);
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        {
             c.captured = true;  // cannot track it: never free it
             return;
         }
-        if (hipEventRecord(c.last, s) != hipSuccess) c.captured = true;
+        if (hipEventRecord(e, s) != hipSuccess)
+        {
+            (void)hipEventDestroy(e);
+            c.captured = true;
+            return;
+        }
+        c.uses.push_back({s, e});
     }
 };
 

@@ -28,3 +28,59 @@ def test_world_size_mismatch_is_refused():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stdout + p.stderr)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_init_timeout_prints_unverified_line_and_exits_nonzero():
+    """rank 0 of a 2-rank job whose peer never starts hangs in the process
+    group's rendezvous; the stage guard prints the line with verified=false and an error naming
+    the stage, and exits non-zero (no retry, no re-exec)."""
+    import json
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--rehearse", "--init-timeout", "6"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    o = json.loads(lines[0])
+    assert o["verified"] is False and o["value"] is None
+    assert o["stage"] == "init_process_group" and "init_process_group" in o["error"]
+    assert o["n_gpus"] == 2 and o["metric"].startswith("device-resident halo pack+unpack")
+
+
+@pytest.mark.parametrize("rank", [0, 1])
+def test_exchange_timeout_prints_unverified_line_and_exits_nonzero(rank):
+    """The same guard around the verified full exchange (the first RCCL traffic between GPUs):
+    a stage that never finishes ends the process with status 3; rank 0 prints the line on
+    stdout, other ranks report on stderr only."""
+    import json
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "g = bench.StageGuard({'metric': bench.METRIC, 'n_gpus': 8}, %d); "
+            "c = g.stage('verified_exchange', 2); c.__enter__(); time.sleep(60)") % (ROOT, rank)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 3
+    out = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    err = [l for l in p.stderr.splitlines() if l.startswith("{")]
+    o = json.loads((out if rank == 0 else err)[0])
+    assert (len(out), len(err)) == ((1, 0) if rank == 0 else (0, 1))
+    assert o["verified"] is False and o["stage"] == "verified_exchange"
+    assert "verified_exchange" in o["error"] and f"rank {rank}" in o["error"]
+
+
+def test_stage_guard_is_silent_when_the_stage_finishes():
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "g = bench.StageGuard({'metric': bench.METRIC}, 0)\n"
+            "with g.stage('init_process_group', 1.5): time.sleep(0.1)\n"
+            "time.sleep(3); print('survived')") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and p.stdout.strip() == "survived"

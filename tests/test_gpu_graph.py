@@ -113,3 +113,63 @@ def test_cached_structured_pack_replayed_from_a_graph():
                                                    (x0, 0, 0), (x1, N - 1, N - 1))
                                         for x0, x1 in ((0, Hw - 1), (N - Hw, N - 1))])
         np.testing.assert_array_equal(buf.cpu().numpy().view(np.uint8), exp)
+
+
+def test_cached_plan_used_on_two_streams_survives_eviction():
+    """a cached plan executed on stream A (held back by a long kernel) and then on
+    stream B, then evicted from the 256-entry cache: it may be freed only once BOTH streams have
+    passed their use, so A's pack still reads valid device tables and writes the right bytes."""
+    import torch
+    from ghex_amd import _ghx
+    N, Hw = 12, 2
+    E = N + 2 * Hw
+    f = torch.arange(E ** 3, dtype=torch.float64, device="cuda").view(E, E, E)
+    d = _ghx.FieldDesc()
+    d.dim, d.elem_size, d.num_components = 3, 8, 1
+    for k in range(3):
+        d.layout[k] = 2 - k
+        d.offsets[k] = Hw
+        d.extents[k] = E
+    d.byte_strides[0], d.byte_strides[1], d.byte_strides[2] = 8, 8 * E, 8 * E * E
+
+    def boxes_of(y1):
+        bx = (_ghx.Box * 2)()
+        for b, (x0, x1) in enumerate(((0, Hw - 1), (N - Hw, N - 1))):
+            bx[b].first[0], bx[b].last[0] = x0, x1
+            bx[b].first[1], bx[b].last[1] = 0, y1
+            bx[b].first[2], bx[b].last[2] = 0, N - 1
+        return bx
+    main = boxes_of(N - 1)
+    buf_a = torch.full((2 * Hw * N * N,), -1.0, dtype=torch.float64, device="cuda")
+    buf_b = torch.full_like(buf_a, -1.0)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    L = _ghx.lib()
+    bp = ctypes.cast(main, ctypes.POINTER(_ghx.Box))
+    with torch.cuda.stream(sa):
+        torch.cuda._sleep(200_000_000)  # hold stream A back while the host evicts the plan
+    _ghx.check(L.ghx_structured_pack(ctypes.byref(d), f.data_ptr(), buf_a.data_ptr(), bp, 2,
+                                     sa.cuda_stream), "pack A")
+    _ghx.check(L.ghx_structured_pack(ctypes.byref(d), f.data_ptr(), buf_b.data_ptr(), bp, 2,
+                                     sb.cuda_stream), "pack B")
+    sb.synchronize()
+    # 300 other keys (other box shapes and halo offsets) push the plan out of the cache and
+    # trigger the reaping of retired plans while stream A has not yet run its pack
+    scratch = torch.empty_like(buf_a)
+    for i in range(300):
+        d2 = _ghx.FieldDesc()
+        ctypes.memmove(ctypes.byref(d2), ctypes.byref(d), ctypes.sizeof(d))
+        d2.offsets[0] = Hw - (i % 2)
+        bx = boxes_of(i % (N - 1))
+        _ghx.check(L.ghx_structured_pack(ctypes.byref(d2), f.data_ptr(), scratch.data_ptr(),
+                                         ctypes.cast(bx, ctypes.POINTER(_ghx.Box)), 2,
+                                         sb.cuda_stream), "evicting pack")
+    sb.synchronize()
+    sa.synchronize()
+    a = f.cpu().numpy()
+    spec = orc.FieldSpec(np.ascontiguousarray(a), 8, (2, 1, 0), (Hw,) * 3, (E,) * 3)
+    exp = np.zeros(buf_a.numel() * 8, dtype=np.uint8)
+    orc.structured_pack(spec, exp, [orc.ISPair((x0, 0, 0), (x1, N - 1, N - 1),
+                                               (x0, 0, 0), (x1, N - 1, N - 1))
+                                    for x0, x1 in ((0, Hw - 1), (N - Hw, N - 1))])
+    np.testing.assert_array_equal(buf_b.cpu().numpy().view(np.uint8), exp)
+    np.testing.assert_array_equal(buf_a.cpu().numpy().view(np.uint8), exp)

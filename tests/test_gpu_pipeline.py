@@ -210,8 +210,20 @@ def test_native_pipeline_one_gpu(rccl_self, N, Hw, doms):
         np.testing.assert_array_equal(a, H.expected_linear_halo(a, d, N, Hw, gl))
     if rccl_self:
         from ghex_amd import _ghx
-        for comm, _ in co._comms.values():
+        comms = dict(ctx._pair_comms)
+        assert comms
+        for comm, _ in comms.values():
             _ghx.call("ghx_rccl_comm_check", comm)
+        # a second communication object of the same context reuses the pair communicators
+        co2 = R.make_communication_object(ctx, pipelined=True, rccl_self=True)
+        co2.exchange(bis).wait()
+        assert {p: c.value for p, (c, _) in ctx._pair_comms.items()} == \
+            {p: c.value for p, (c, _) in comms.items()}
+        del co, co2
+        import gc
+        gc.collect()
+        ctx.close()
+        assert not ctx._pair_comms
 
 
 def test_unstructured_cache_sees_in_place_change():
