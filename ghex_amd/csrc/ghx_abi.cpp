@@ -449,8 +449,7 @@ void build_mixed(exchange_plan& ex, int32_t me, const std::vector<ghx_pack_entry
         if (m >= su.host_segs.size()) return;
         const seg_s& q = su.host_segs[m++];
         if (q.buf_slot != ps[k].buf_slot || q.buf_off != ps[k].buf_off || q.bytes != ps[k].bytes ||
-            q.row_bytes != ps[k].row_bytes || q.tile_bytes != ps[k].tile_bytes ||
-            ps[k].partner >= 0 || q.bytes == 0)
+            q.row_bytes != ps[k].row_bytes || q.tile_bytes != ps[k].tile_bytes || q.bytes == 0)
             return;
         comp[k] = q;
     }
@@ -486,30 +485,10 @@ int ghx_tune(const char* key, int32_t value)
         const std::string k(key);
         if (k == "reset")
             g_tune = tuning{};
-        else if (k == "unroll")
-        {
-            if (value != 2 && value != 4 && value != 8) throw invalid("unroll must be 2, 4 or 8");
-            g_tune.unroll = value;
-        }
-        else if (k == "nt")
-        {
-            if (value < 0 || value > 3) throw invalid("nt must be 0, 1, 2 or 3");
-            g_tune.nt = value;
-        }
-        else if (k == "nt_dir")
-        {
-            if (value < 0 || value > 2) throw invalid("nt_dir must be 0, 1 or 2");
-            g_tune.nt_dir = value;
-        }
         else if (k == "order")
         {
-            if (value < 0 || value > 4) throw invalid("order must be in 0..4");
+            if (value < 0 || value > 1) throw invalid("order must be 0 or 1");
             g_tune.order = value;
-        }
-        else if (k == "pair")
-        {
-            if (value < 0 || value > 2) throw invalid("pair must be 0, 1 or 2");
-            g_tune.pair = value;
         }
         else if (k == "self_tile_bytes")
         {
@@ -517,40 +496,10 @@ int ghx_tune(const char* key, int32_t value)
                 throw invalid("self_tile_bytes must be a power of two in [1 KiB, 1 MiB]");
             g_tune.self_tile_bytes = uint32_t(value);
         }
-        else if (k == "self_chunk")
-        {
-            if (value < 0 || (value & 15)) throw invalid("self_chunk must be a multiple of 16 (0: tile)");
-            g_tune.self_chunk = uint32_t(value);
-        }
-        else if (k == "self_pipe")
-        {
-            if (value < 0 || value > 2) throw invalid("self_pipe must be 0, 1 or 2");
-            g_tune.self_pipe = value;
-        }
-        else if (k == "self_lane_local")
-        {
-            if (value < 0 || value > 2) throw invalid("self_lane_local must be 0, 1 or 2");
-            g_tune.self_lane_local = value;
-        }
         else if (k == "mixed_always")
         {
             if (value < 0 || value > 1) throw invalid("mixed_always must be 0 or 1");
             g_tune.mixed_always = value;
-        }
-        else if (k == "xcd_rotate")
-        {
-            if (value < 0 || value > 2) throw invalid("xcd_rotate must be 0, 1 or 2");
-            g_tune.xcd_rotate = value;
-        }
-        else if (k == "lds")
-        {
-            if (value < 0 || value > 1) throw invalid("lds must be 0 or 1");
-            g_tune.lds = value;
-        }
-        else if (k == "short_xcds")
-        {
-            if (value < 0 || value > 7) throw invalid("short_xcds must be in 0..7");
-            g_tune.short_xcds = value;
         }
         else if (k == "xcd_pair")
         {
@@ -571,11 +520,6 @@ int ghx_tune(const char* key, int32_t value)
         {
             if (value < 4) throw invalid("u_run_tile_rows must be >= 4");
             g_tune.u_run_tile_rows = uint32_t(value);
-        }
-        else if (k == "usort")
-        {
-            if (value < 0 || value > 1) throw invalid("usort must be 0 or 1");
-            g_tune.usort = value;
         }
         else if (k == "short_pol")
         {
@@ -1173,10 +1117,6 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
         kargs a{};
         a.segs = p.dev.segs;
         a.segs2 = q.dev.segs;
-        a.chunk = g_tune.self_chunk;
-        a.lane_local = uint32_t(g_tune.self_lane_local);
-        // 1: short-row (x-face) tiles only, 2: every tile
-        a.pipe = g_tune.self_pipe == 2 ? 0xFFFFFFFFu : g_tune.self_pipe ? g_tune.small_row_bytes : 0u;
         a.tile_seg = p.dev.tiles;
         a.n_tiles = p.n_tiles;
         for (int i = 0; i <= p.max_field_slot; ++i)
@@ -1217,9 +1157,6 @@ int ghx_exchange_pack_self(const ghx_exchange* ex, void* const* field_ptrs, int3
         kargs a{};
         a.segs = p.dev.segs;
         a.segs2 = ex->mixed_comp.segs;
-        a.chunk = g_tune.self_chunk;
-        a.lane_local = uint32_t(g_tune.self_lane_local);
-        a.pipe = 0;
         a.tile_seg = p.dev.tiles;
         a.n_tiles = p.n_tiles;
         for (int i = 0; i <= p.max_field_slot; ++i)
@@ -1304,20 +1241,7 @@ int ghx_put_create(const ghx_pack_entry* src, int32_t n_src, const ghx_pack_entr
         *out = nullptr;
         if (n_src < 0 || n_dst < 0 || (n_src && !src) || (n_dst && !dst))
             throw invalid("bad entry arrays");
-        const int saved_pair = g_tune.pair;
-        g_tune.pair = 0;  // partner segments have no counterpart on the other side
-        std::unique_ptr<ghx_put> p;
-        try
-        {
-            p.reset(new ghx_put(src, n_src, dst, n_dst));
-        }
-        catch (...)
-        {
-            g_tune.pair = saved_pair;
-            throw;
-        }
-        g_tune.pair = saved_pair;
-        *out = p.release();
+        *out = new ghx_put(src, n_src, dst, n_dst);
         return GHX_OK;
     });
 }

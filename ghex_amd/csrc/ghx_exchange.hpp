@@ -109,8 +109,7 @@ struct exchange_plan
             const auto& a = p.host_segs[k];
             const auto& b = q.host_segs[k];
             ok = a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
-                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes && a.partner < 0 &&
-                 b.partner < 0;
+                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes;
         }
         return ok;
     }

@@ -23,66 +23,33 @@ constexpr uint32_t kTileBytes = 8192;
 constexpr uint32_t kMaxTileBytes = 1u << 20;
 constexpr int kBlock = 256;
 
-// Launch / planning knobs (ghx_tune). Defaults are the measured best.
+// Launch / planning knobs (ghx_tune). Defaults are the measured best. The knobs
+// whose every setting but the default lost its A/B were removed in round 3
+// (tools/kernel_variants_r02.hip lists them with their numbers).
 struct tuning
 {
-    int unroll = 4;                 // vectors in flight per lane per loop trip: 2, 4, 8
-    int nt = 0;                     // 0 default, 1 nt stores, 2 nt loads + stores, 3 nt loads
-    int nt_dir = 0;                 // nt applies to: 0 both directions, 1 pack, 2 unpack
     int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
     uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
     uint32_t self_tile_bytes = kTileBytes;  // the same for the fused self exchange (separate
                                        // self plans are built when it differs). Medians of 4
-                                       // interleaved A/B runs with register forwarding
-                                       // (self_lane_local 2): H=2 8 KiB 26.4 vs 4 KiB 27.9 us;
-                                       // H=1 18.6 vs 19.9; H=3 32.8 vs 32.0
-                                       // (profiles/r01c_fwd_tile_ab.jsonl)
+                                       // interleaved A/B runs with register forwarding:
+                                       // H=2 8 KiB 26.4 vs 4 KiB 27.9 us; H=1 18.6 vs 19.9;
+                                       // H=3 32.8 vs 32.0 (profiles/r01c_fwd_tile_ab.jsonl)
     uint32_t small_tile_rows = 4096;   // rows per tile of segments with short rows
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
     int order = 1;                     // tile dispatch order: 0 segment order, 1 short-row
-                                       // segments first, 2 round-robin over segments, 3 the
-                                       // short-row units spread evenly among the long ones,
-                                       // 4 short-row units last
-    int pair = 0;                      // pair short-row segments whose rows interleave in
-                                       // memory (the +x face of row y and the -x face of row
-                                       // y+1 share a cache line): 1 one lane moves both, 2 the
-                                       // two rows of a line go to adjacent lanes of one wave
-                                       // instruction (copy_tile_ilv). 1 is off by default: with
-                                       // short-row-first dispatch the L2 already merges the
-                                       // shared-line misses (same TCC_EA0_RDREQ)
+                                       // segments first (2-4 lost: tools/kernel_variants_r02.hip)
     int urun = 1;                      // unstructured 4/8-B-row segments: 16-B lane chunks with
                                        // run detection (copy_runs)
     uint32_t u_run_tile_rows = 2048;   // rows per tile of run-heavy index-list segments
-    int usort = 0;                     // unstructured one-row-per-index segments: visit the
-                                       // indices in ascending field order (buffer side
-                                       // scattered through a permutation)
     int short_pol = 0;                 // field-side cache policy of short-row segments:
                                        // bit 0 non-temporal loads (pack), bit 1 sc1 stores
                                        // (unpack)
-    uint32_t self_chunk = 0;           // fused self exchange: a workgroup packs, then unpacks,
-                                       // this many buffer bytes at a time (0: the whole tile;
-                                       // 4-32 KiB chunks measured no faster, 4 KiB slower)
-    int self_pipe = 0;                 // fused self exchange: software-pipelined tiles (the
-                                       // x-face halo stores overlap the next chunk's loads);
-                                       // 1 short-row tiles, 2 all. Measured: H=2 within noise,
-                                       // H=1 +3 %, H=3 +12 % time -> off
-    int self_lane_local = 2;           // fused self exchange without the intra-tile barrier
-                                       // when both halves use the same vector width; 2: the
-                                       // unpack half takes the packed bytes from registers
-                                       // (self_forward) instead of reading the buffer back
     int xcd_pair = 1;                  // dispatch the tiles of line-sharing short-row segment
                                        // pairs in lock-step groups of 8, so tile t of both
                                        // halves lands on the same XCD (blocks are dealt
                                        // round-robin over the 8 XCDs) at the same time
-    int xcd_rotate = 0;                // line-sharing pair groups dealt to the XCDs rotated by
-                                       // the group index (balances the L2 channels per XCD)
-    int lds = 0;                       // 1: pack 8/16-B rows through LDS (copy_tile_lds:
-                                       // whole 64-B blocks read four lanes each, pieces
-                                       // extracted one row per lane)
-    int short_xcds = 0;                // >0 (1..7): deal the short-row tiles to the first this
-                                       // many XCDs only (block b on XCD b mod 8), the other
-                                       // XCDs' L2s stream the long rows meanwhile
     int mixed_always = 0;              // build the mixed self/peer plans even when the self
                                        // messages hold no short rows (tests, measurements)
 };
@@ -129,8 +96,7 @@ struct alignas(16) seg_s
     uint8_t fpol;         // field-side cache policy: bit 0 nt loads, bit 1 sc1 stores
     uint8_t pad1;
     uint32_t tile_bytes;  // this segment's tile size (a multiple of the row length or 16 KiB)
-    int32_t partner;      // paired segment (row r here travels with its row r-1), or -1
-    uint8_t pad[4];
+    uint8_t pad[8];
 };
 static_assert(sizeof(seg_s) == 128, "seg_s layout");
 
@@ -157,7 +123,7 @@ struct alignas(16) seg_u
     uint8_t lid64;
     uint8_t fpol;              // field-side cache policy (as seg_s)
     uint32_t tile_bytes;
-    const uint32_t* perm;      // mode 0, sorted: lids ascending, perm[k] = buffer row of lid k
+    uint64_t reserved;
     uint8_t runs;              // mode 0, rows of 4 or 8 B, rows of consecutive lids contiguous
                                // in the field: lanes move 16-B chunks (16/L rows), one 16-B
                                // field access where the chunk's lids form a run (copy_runs);
@@ -173,11 +139,6 @@ struct kargs
     const void* segs2;         // fused self exchange: the unpack segments (1:1 with segs)
     const uint32_t* tile_seg;  // per tile: {segment index, tile index within the segment}
     uint32_t n_tiles;
-    uint32_t chunk;            // fused self exchange: pack/unpack alternate per chunk (0: tile)
-    uint32_t pipe;             // fused self exchange: tiles with rows shorter than this many
-                               // bytes are software-pipelined (self_pipelined)
-    uint32_t lane_local;       // fused self exchange: no barrier when pack and unpack of a tile
-                               // map lanes to buffer bytes identically
     uint64_t field_ptr[GHX_MAX_SLOTS];
     uint64_t buf_ptr[GHX_MAX_SLOTS];
 };
@@ -187,7 +148,7 @@ void set_error(const std::string& msg);
 const char* get_error();
 
 // kernel launchers (ghx_kernels.hip)
-int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid, int pairs);
+int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid);
 int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid, bool runs);
 int launch_self(const kargs& a, void* stream, uint32_t grid);
 int launch_put(const kargs& a, void* stream, uint32_t grid);

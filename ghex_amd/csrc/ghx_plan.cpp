@@ -33,12 +33,12 @@ std::vector<int32_t> line_partners(const std::vector<seg_s>& segs)
     for (size_t i = 0; i < segs.size(); ++i)
     {
         const auto& a = segs[i];
-        if (partner[i] >= 0 || a.partner >= 0 || a.row_bytes >= g_tune.small_row_bytes ||
+        if (partner[i] >= 0 || a.row_bytes >= g_tune.small_row_bytes ||
             a.n_outer < 1 || a.bytes / a.row_bytes < 2)
             continue;
         for (size_t j = 0; j < segs.size(); ++j)
         {
-            if (j == i || partner[j] >= 0 || segs[j].partner >= 0) continue;
+            if (j == i || partner[j] >= 0) continue;
             const auto& b = segs[j];
             bool same = b.field_slot == a.field_slot && b.row_bytes == a.row_bytes &&
                         b.n_outer == a.n_outer && b.bytes == a.bytes;
@@ -74,12 +74,11 @@ uint32_t short_tile_rows(const seg_u& s)
 // (request-bound: one memory request per row) may use a different tile size from streaming
 // segments; the dispatch order of tiles is a tuning knob (hardware dispatches in blockIdx order).
 template<typename Seg>
-std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char>* skip = nullptr)
+std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
 {
     std::vector<std::vector<uint32_t>> per(segs.size());
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
-        if (skip && (*skip)[i]) continue;  // moved by its pair partner's tiles
         const bool small = segs[i].row_bytes < g_tune.small_row_bytes;
         uint32_t tb = g_tune.tile_bytes;
         if (small)
@@ -102,219 +101,41 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, const std::vector<char
         out.push_back(i);
         out.push_back(t);
     };
-    if (g_tune.order == 2)
+    std::vector<uint32_t> idx(segs.size());
+    for (uint32_t i = 0; i < segs.size(); ++i) idx[i] = i;
+    if (g_tune.order == 1)
+        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+            return (segs[a].row_bytes < g_tune.small_row_bytes) >
+                   (segs[b].row_bytes < g_tune.small_row_bytes);
+        });
+    std::vector<int32_t> partner(segs.size(), -1);
+    if (g_tune.order == 1 && g_tune.xcd_pair) partner = line_partners(segs);
+    // Line-sharing pairs first, in lock-step groups of 8 tiles: tile t of one half at block
+    // 16k + i, tile t of the other at 16k + 8 + i -> the same XCD (blocks are dealt
+    // round-robin over the 8 XCDs) at about the same time, so each shared line is fetched
+    // once into that XCD's L2 and both halves' partial writes merge there. A short group is
+    // padded with tiles of the other segments so the alignment holds.
+    std::vector<std::pair<uint32_t, uint32_t>> rest;
+    for (uint32_t i : idx)
+        if (partner[i] < 0)
+            for (uint32_t t : per[i]) rest.emplace_back(i, t);
+    size_t next = 0;
+    for (uint32_t i : idx)
     {
-        // round-robin over segments
-        size_t maxn = 0;
-        for (auto& v : per) maxn = std::max(maxn, v.size());
-        for (size_t k = 0; k < maxn; ++k)
-            for (uint32_t i = 0; i < segs.size(); ++i)
-                if (k < per[i].size()) emit(i, per[i][k]);
-    }
-    else
-    {
-        std::vector<uint32_t> idx(segs.size());
-        for (uint32_t i = 0; i < segs.size(); ++i) idx[i] = i;
-        if (g_tune.order == 1 || g_tune.order >= 3)
-            std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
-                return (segs[a].row_bytes < g_tune.small_row_bytes) >
-                       (segs[b].row_bytes < g_tune.small_row_bytes);
-            });
-        std::vector<int32_t> partner(segs.size(), -1);
-        if ((g_tune.order == 1 || g_tune.order >= 3) && g_tune.xcd_pair && !g_tune.pair)
-            partner = line_partners(segs);
-        // Line-sharing pairs first, in lock-step groups of 8 tiles: tile t of one half at block
-        // 16k + i, tile t of the other at 16k + 8 + i -> the same XCD (blocks are dealt
-        // round-robin over the 8 XCDs) at about the same time, so each shared line is fetched
-        // once into that XCD's L2 and both halves' partial writes merge there. A short group is
-        // padded with tiles of the other segments so the alignment holds.
-        std::vector<std::pair<uint32_t, uint32_t>> rest;
-        for (uint32_t i : idx)
-            if (partner[i] < 0)
-                for (uint32_t t : per[i]) rest.emplace_back(i, t);
-        size_t next = 0;
-        for (uint32_t i : idx)
+        const int32_t j = partner[i];
+        if (j < 0 || uint32_t(j) < i) continue;
+        const size_t n = per[i].size();  // == per[j].size(): partners have equal bytes
+        for (size_t k = 0; k < n; k += 8)
         {
-            const int32_t j = partner[i];
-            if (j < 0 || uint32_t(j) < i || per[i].size() != per[size_t(j)].size())
-            {
-                if (j >= 0 && per[i].size() != per[size_t(j)].size())
-                    for (uint32_t t : per[i]) emit(i, t);  // (cannot happen: equal bytes)
-                continue;
-            }
-            const size_t n = per[i].size();
-            for (size_t k = 0; k < n; k += 8)
-            {
-                const size_t m = std::min<size_t>(8, n - k);
-                // xcd_rotate: group g deals its tiles to the XCDs rotated by g, so an XCD's tiles
-                // come from every residue of the tile index (the L2 channel a line maps to varies
-                // with high address bits: with tiles dealt in plain order each XCD would see the
-                // same few channels over and over)
-                size_t pos[8];
-                for (size_t u = 0; u < m; ++u) pos[u] = g_tune.xcd_rotate == 1 ? (u + k / 8) % m : u;
-                if (g_tune.xcd_rotate == 2)  // a pseudo-random order per group (fixed seed)
-                {
-                    uint64_t x = 0x9e3779b97f4a7c15ull * (k / 8 + 1);
-                    for (size_t u = m; u > 1; --u)
-                    {
-                        x ^= x >> 33;
-                        x *= 0xff51afd7ed558ccdull;
-                        x ^= x >> 33;
-                        std::swap(pos[u - 1], pos[x % u]);
-                    }
-                }
-                for (size_t u = 0; u < m; ++u) emit(uint32_t(j), per[size_t(j)][k + pos[u]]);
-                for (size_t u = m; u < 8 && next < rest.size(); ++u, ++next)
-                    emit(rest[next].first, rest[next].second);
-                for (size_t u = 0; u < m; ++u) emit(i, per[i][k + pos[u]]);
-            }
-        }
-        for (; next < rest.size(); ++next) emit(rest[next].first, rest[next].second);
-        if (g_tune.short_xcds > 0 && g_tune.order == 1)
-        {
-            // short-row tiles only at blocks b with b mod 8 < short_xcds (blocks are dealt
-            // round-robin over the 8 XCDs), long-row tiles in the other slots; the k-th tiles of
-            // both halves of a line-sharing pair keep equal (k mod short_xcds) -> same XCD
-            const uint32_t X = uint32_t(g_tune.short_xcds);
-            std::vector<uint32_t> sh, lo, mix;
-            for (size_t k = 0; k < out.size(); k += 2)
-            {
-                auto& dst = segs[out[k]].row_bytes < g_tune.small_row_bytes ? sh : lo;
-                dst.push_back(out[k]);
-                dst.push_back(out[k + 1]);
-            }
-            size_t a = 0, b = 0;
-            for (uint32_t blk = 0; a < sh.size() || b < lo.size(); ++blk)
-            {
-                const bool want_short = (blk % 8) < X;
-                auto& src = (want_short && a < sh.size()) || b >= lo.size() ? sh : lo;
-                size_t& at = &src == &sh ? a : b;
-                mix.push_back(src[at]);
-                mix.push_back(src[at + 1]);
-                at += 2;
-            }
-            out.swap(mix);
-        }
-        if (g_tune.order == 4)
-        {
-            // long-row units first, the short-row units (16-block groups) after them
-            const size_t nt = out.size() / 2, U = 16;
-            std::vector<uint32_t> sh, lo;
-            for (size_t t = 0; t < nt; t += U)
-            {
-                const size_t e = std::min(nt, t + U);
-                bool any_short = false;
-                for (size_t k = t; k < e; ++k)
-                    any_short = any_short || segs[out[2 * k]].row_bytes < g_tune.small_row_bytes;
-                auto& dst = any_short ? sh : lo;
-                dst.insert(dst.end(), out.begin() + std::ptrdiff_t(2 * t), out.begin() + std::ptrdiff_t(2 * e));
-            }
-            lo.insert(lo.end(), sh.begin(), sh.end());
-            out.swap(lo);
-        }
-        if (g_tune.order == 3)
-        {
-            // spread: the short-row units (16 consecutive blocks, so lock-step pair groups stay
-            // aligned) dealt evenly among the long-row units instead of all first, so that every
-            // stretch of the launch mixes request-bound and streaming tiles
-            const size_t nt = out.size() / 2, U = 16;
-            std::vector<std::pair<size_t, size_t>> sh, lo;  // [first tile, end tile)
-            for (size_t t = 0; t < nt; t += U)
-            {
-                const size_t e = std::min(nt, t + U);
-                bool any_short = false;
-                for (size_t k = t; k < e; ++k)
-                    any_short = any_short || segs[out[2 * k]].row_bytes < g_tune.small_row_bytes;
-                (any_short ? sh : lo).emplace_back(t, e);
-            }
-            std::vector<uint32_t> spread;
-            spread.reserve(out.size());
-            auto put = [&](std::pair<size_t, size_t> u) {
-                for (size_t k = u.first; k < u.second; ++k)
-                {
-                    spread.push_back(out[2 * k]);
-                    spread.push_back(out[2 * k + 1]);
-                }
-            };
-            size_t li = 0;
-            for (size_t si = 0; si < sh.size(); ++si)
-            {
-                const size_t upto = (si * lo.size()) / std::max<size_t>(1, sh.size());
-                for (; li < upto; ++li) put(lo[li]);
-                put(sh[si]);
-            }
-            for (; li < lo.size(); ++li) put(lo[li]);
-            out.swap(spread);
+            const size_t m = std::min<size_t>(8, n - k);
+            for (size_t u = 0; u < m; ++u) emit(uint32_t(j), per[size_t(j)][k + u]);
+            for (size_t u = m; u < 8 && next < rest.size(); ++u, ++next)
+                emit(rest[next].first, rest[next].second);
+            for (size_t u = 0; u < m; ++u) emit(i, per[i][k + u]);
         }
     }
+    for (; next < rest.size(); ++next) emit(rest[next].first, rest[next].second);
     return out;
-}
-
-int wlog2_seg(const seg_s& s)
-{
-    int w = wlog2_of(uint64_t(s.row_bytes));
-    w = std::min(w, wlog2_of(uint64_t(s.field_off)));
-    w = std::min(w, wlog2_of(s.buf_off));
-    for (int k = 0; k < s.n_outer; ++k)
-        if (s.ext[k] > 1)
-            w = std::min(w, wlog2_of(uint64_t(s.stride[k] < 0 ? -s.stride[k] : s.stride[k])));
-    return w;
-}
-
-// Pair short-row segments of one field whose rows interleave in memory: row r of the primary P
-// and row r-1 of the partner Q lie within one 128 B line when
-// 0 < P.field_off + P.stride[0] - Q.field_off < 128 (for unpadded rows of a structured field:
-// the +x face of row y ends 48 B before the -x face of row y+1 starts at H=2). One lane then
-// moves both pieces, so their shared line is requested once instead of twice. Q's last row has
-// no primary row after it and becomes a 1-row tail segment. Returns the consumed mask.
-std::vector<char> pair_segments(std::vector<seg_s>& segs)
-{
-    std::vector<char> consumed(segs.size(), 0);
-    const size_t n0 = segs.size();
-    for (size_t i = 0; i < n0; ++i)
-    {
-        auto& p = segs[i];
-        if (consumed[i] || p.partner >= 0 || p.row_bytes >= g_tune.small_row_bytes || p.n_outer < 1)
-            continue;
-        for (size_t j = 0; j < n0; ++j)
-        {
-            if (j == i || consumed[j] || segs[j].partner >= 0) continue;
-            const auto& q = segs[j];
-            bool same = q.field_slot == p.field_slot && q.row_bytes == p.row_bytes &&
-                        q.n_outer == p.n_outer && q.bytes == p.bytes && q.wlog2 == p.wlog2;
-            for (int k = 0; same && k < 4; ++k)
-                same = q.ext[k] == p.ext[k] && q.stride[k] == p.stride[k];
-            if (!same || p.bytes / p.row_bytes < 2) continue;
-            const int64_t d = p.field_off + p.stride[0] - q.field_off;
-            if (d <= 0 || d >= 128 || d < int64_t(p.row_bytes)) continue;  // disjoint, one line
-            bool taken = false;
-            for (size_t k = 0; k < n0 && !taken; ++k) taken = segs[k].partner == int32_t(j);
-            if (taken) continue;
-            p.partner = int32_t(j);
-            consumed[j] = 1;
-            // tail: Q's last row (r = R-1)
-            seg_s t = q;
-            int64_t off = 0;
-            for (int k = 0; k < 4; ++k) off += int64_t(q.ext[k] - 1) * q.stride[k];
-            const uint32_t R = q.bytes / q.row_bytes;
-            t.field_off = q.field_off + off;
-            t.buf_off = q.buf_off + uint64_t(R - 1) * q.row_bytes;
-            for (int k = 0; k < 4; ++k)
-            {
-                t.ext[k] = 1;
-                t.stride[k] = 0;
-            }
-            for (int k = 0; k < 3; ++k) t.mag_ext[k] = make_magic(1);
-            t.n_outer = 0;
-            t.bytes = q.row_bytes;
-            t.partner = -1;
-            t.wlog2 = uint8_t(wlog2_seg(t));
-            segs.push_back(t);
-            consumed.push_back(0);
-            break;
-        }
-    }
-    return consumed;
 }
 
 bool have_device()
@@ -471,7 +292,6 @@ uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, cons
     {
         const int64_t cnt = std::min(chunk, nslow - s0);
         seg_s s{};
-        s.partner = -1;
         s.field_slot = field_slot;
         s.buf_slot = buf_slot;
         s.row_bytes = uint32_t(L);
@@ -528,13 +348,9 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
                                     uint16_t(en.buffer_slot), off);
         bytes += off - en.buffer_offset;
     }
-    std::vector<char> consumed;
-    if (g_tune.pair) consumed = pair_segments(segs);
-    std::vector<uint32_t> tiles = build_tiles(segs, g_tune.pair ? &consumed : nullptr);
+    std::vector<uint32_t> tiles = build_tiles(segs);
     n_segments = int32_t(segs.size());
     n_tiles = uint32_t(tiles.size() / 2);
-    for (const seg_s& s : segs)
-        if (s.partner >= 0) has_pairs = g_tune.pair == 2 ? 2 : 1;
     host_segs = segs;
     upload(dev, segs, tiles);
 }
@@ -558,7 +374,7 @@ int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
         if (!bptr[i]) throw invalid("null buffer pointer");
         a.buf_ptr[i] = reinterpret_cast<uint64_t>(bptr[i]);
     }
-    return launch_structured(a, direction, stream, grid_for_tiles(n_tiles), has_pairs);
+    return launch_structured(a, direction, stream, grid_for_tiles(n_tiles));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -577,8 +393,6 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         int64_t n;
         bool wide;
         size_t off;
-        bool sorted = false;   // store lids ascending + the buffer-row permutation
-        size_t perm_off = 0;
     };
     std::vector<pending> pend;
     size_t lid_bytes = 0;
@@ -659,15 +473,6 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         lid_bytes = (lid_bytes + 15) & ~size_t(15);
         pending pe{segs.size(), en.lids, en.n_lids, wide, lid_bytes};
         lid_bytes += size_t(en.n_lids) * (wide ? 8 : 4);
-        if (g_tune.usort && s.mode == 0 && en.n_lids >= 256 &&
-            !std::is_sorted(en.lids, en.lids + en.n_lids))
-        {
-            lid_bytes = (lid_bytes + 15) & ~size_t(15);
-            s.runs = 0;  // the buffer side goes through perm
-            pe.sorted = true;
-            pe.perm_off = lid_bytes;
-            lid_bytes += size_t(en.n_lids) * 4;
-        }
         pend.push_back(pe);
         segs.push_back(s);
         bytes += uint64_t(total);
@@ -681,36 +486,21 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         std::vector<unsigned char> host(lid_bytes);
         for (auto& p : pend)
         {
-            std::vector<uint32_t> order;
-            if (p.sorted)
-            {
-                order.resize(size_t(p.n));
-                for (int64_t i = 0; i < p.n; ++i) order[size_t(i)] = uint32_t(i);
-                std::stable_sort(order.begin(), order.end(),
-                                 [&](uint32_t a, uint32_t b) { return p.lids[a] < p.lids[b]; });
-                std::memcpy(host.data() + p.perm_off, order.data(), size_t(p.n) * 4);
-            }
-            auto lid_at = [&](int64_t k) { return p.sorted ? p.lids[order[size_t(k)]] : p.lids[k]; };
             if (p.wide)
             {
                 int64_t* dst = reinterpret_cast<int64_t*>(host.data() + p.off);
-                for (int64_t i = 0; i < p.n; ++i) dst[i] = lid_at(i);
+                for (int64_t i = 0; i < p.n; ++i) dst[i] = p.lids[i];
             }
             else
             {
                 int32_t* dst = reinterpret_cast<int32_t*>(host.data() + p.off);
-                for (int64_t i = 0; i < p.n; ++i) dst[i] = int32_t(lid_at(i));
+                for (int64_t i = 0; i < p.n; ++i) dst[i] = int32_t(p.lids[i]);
             }
         }
         if (hipMalloc(&dev.lids, lid_bytes) != hipSuccess) throw hip_error("hipMalloc(lids)");
         if (hipMemcpy(dev.lids, host.data(), lid_bytes, hipMemcpyHostToDevice) != hipSuccess)
             throw hip_error("hipMemcpy(lids)");
-        for (auto& p : pend)
-        {
-            segs[p.seg].lids = static_cast<char*>(dev.lids) + p.off;
-            if (p.sorted)
-                segs[p.seg].perm = reinterpret_cast<const uint32_t*>(static_cast<char*>(dev.lids) + p.perm_off);
-        }
+        for (auto& p : pend) segs[p.seg].lids = static_cast<char*>(dev.lids) + p.off;
         void* keep = dev.lids;
         dev.lids = nullptr;  // upload() releases; re-attach after
         upload(dev, segs, tiles);

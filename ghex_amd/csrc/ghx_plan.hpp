@@ -45,8 +45,6 @@ struct splan
     uint32_t n_tiles = 0;
     uint32_t tile_bytes = kTileBytes;
     int max_field_slot = -1, max_buf_slot = -1;
-    int has_pairs = 0;  // segments paired by pair_segments (knob "pair"): k_copy<..., PAIR>;
-                        // 2: interleaved lanes (k_copy<..., PAIR, ILV>)
     std::vector<seg_s> host_segs;
     device_tables dev;
     splan(const ghx_pack_entry* entries, int n_entries, int direction);

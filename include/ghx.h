@@ -44,24 +44,18 @@ typedef void* ghx_stream;
 #define GHX_MAX_SLOTS 64  /* field / buffer pointer slots per plan execution */
 
 /* Process-wide tuning knobs (development / benchmarking; defaults are the measured best):
- * "unroll" (2|4|8 vectors in flight per lane), "nt" (0 default cache policy, 1 non-temporal
- * stores, 2 non-temporal loads and stores, 3 non-temporal loads), "nt_dir" (0|1|2: "nt" applies
- * to both directions, the pack only, the unpack only), "grid_cap" (max workgroups, 0 = one per tile),
- * "tile_bytes" (buffer bytes per workgroup tile), "small_tile_rows", "small_row_bytes",
- * "u_tile_rows" (rows per tile of short-row index-list segments), "usort" (0|1: visit index
- * lists in ascending field order),
- * "order" (0 segment order, 1 short-row segments first, 2 round-robin), "pair" (0|1),
- * "short_pol" (field-side cache policy of short-row segments: bit 0 non-temporal loads,
- * bit 1 sc1 stores), "xcd_pair" (0|1: line-sharing short-row segment pairs dispatched in
- * lock-step groups of 8 tiles, same XCD), "short_xcds" (0..7: short-row tiles dealt to the
- * first this many XCDs only, 0 = all), "xcd_rotate" (0|1|2: pair groups dealt to the XCDs in
- * order, rotated by the group index, or in a pseudo-random order), "lds" (0|1: pack 8/16-B rows staged through LDS as
- * whole 64-B blocks), "urun" (0|1: run path for 4/8-B index-list rows),
- * "u_run_tile_rows" (rows per tile of run-heavy index lists); fused self exchange:
- * "self_tile_bytes", "self_lane_local" (0|1: pack->unpack hand-off inside each lane, no
- * workgroup barrier), "self_chunk" (bytes per pack/unpack alternation, 0 = tile), "self_pipe"
- * (0|1|2 software-pipelined tiles); "reset" restores every default. Plan-shaping knobs apply to
- * plans created afterwards.
+ * "grid_cap" (max workgroups, 0 = one per tile), "tile_bytes" (buffer bytes per workgroup tile),
+ * "small_tile_rows" (rows per tile of short-row structured segments), "small_row_bytes" (rows
+ * shorter than this are "short"), "order" (0 segment order, 1 short-row segments first),
+ * "xcd_pair" (0|1: line-sharing short-row segment pairs dispatched in lock-step groups of 8
+ * tiles, same XCD), "short_pol" (field-side cache policy of short-row segments: bit 0
+ * non-temporal loads, bit 1 sc1 stores), "u_tile_rows" (rows per tile of short-row index-list
+ * segments), "urun" (0|1: run path for 4/8-B index-list rows), "u_run_tile_rows" (rows per tile
+ * of run-heavy index lists), "self_tile_bytes" (tile of the fused self exchange),
+ * "mixed_always" (0|1: build mixed self/peer plans even without short-row self messages);
+ * "reset" restores every default. Plan-shaping knobs apply to plans created afterwards. Unknown
+ * keys fail with GHX_ERR_INVALID (the variants removed in round 3 are listed in
+ * tools/kernel_variants_r02.hip).
  * No reference counterpart (the reference hard-codes block_dim=128, 1 element per thread:
  * include/ghex/structured/pack_kernels.hpp:211-214). */
 int ghx_tune(const char* key, int32_t value);

@@ -71,18 +71,11 @@ def _random_lists(rng, n_cells, n_halo, peers):
     return np.split(send, cuts), np.split(rng.permutation(recv), cuts)
 
 
-@pytest.mark.parametrize("levels,levels_first,usort", [(1, True, 0), (1, True, 1), (8, True, 0),
-                                                      (8, True, 1), (8, False, 0), (3, False, 0)])
-def test_config5_unstructured_10M(levels, levels_first, usort):
+@pytest.mark.parametrize("levels,levels_first", [(1, True), (8, True), (8, False), (3, False)])
+def test_config5_unstructured_10M(levels, levels_first):
     """10M cells, 5% halo, 7 peers; fused gather (pack) and scatter (unpack) of every peer's
-    index list vs the oracle's data_descriptor get/set, bit-exact; usort=1 visits the indices in
-    ascending field order (buffer side through the permutation)."""
-    from ghex_amd import _ghx
-    _ghx.call("ghx_tune", b"usort", usort)
-    try:
-        _config5_case(levels, levels_first)
-    finally:
-        _ghx.call("ghx_tune", b"reset", 0)
+    index list vs the oracle's data_descriptor get/set, bit-exact."""
+    _config5_case(levels, levels_first)
 
 
 def _config5_case(levels, levels_first):

@@ -106,6 +106,7 @@ def main():
             e1.record()
             _ghx.call("ghx_launch_timing_read", ms, n, ctypes.byref(got))
             _ghx.call("ghx_launch_timing", 0)
+            e1.synchronize()
             durs.append((e0.elapsed_time(e1) * 1e3, [ms[i] * 1e3 for i in range(got.value)]))
         seqt = sorted(d for d, _ in durs)
         per = [sorted(k[i] for _, k in durs if len(k) == len(kern)) for i in range(len(kern))]
