@@ -118,6 +118,12 @@ _SIGS = {
     "ghx_put_execute": (c_i32, [c_vp, P(c_vp), c_i32, P(c_vp), c_i32, c_vp]),
     "ghx_put_info": (c_i32, [c_vp, P(ctypes.c_uint64), P(c_i32)]),
     "ghx_put_destroy": (c_i32, [c_vp]),
+    "ghx_epochs_create": (c_i32, [ctypes.c_char_p, c_i32, c_i32, c_i32, ctypes.c_double, P(c_vp)]),
+    "ghx_epochs_unlink": (c_i32, [ctypes.c_char_p]),
+    "ghx_epochs_peers": (c_i32, [c_vp, P(c_i32), c_i32, P(c_i32), c_i32]),
+    "ghx_epochs_enqueue": (c_i32, [c_vp, c_i32, c_vp]),
+    "ghx_epochs_status": (c_i32, [c_vp, P(c_i32), P(ctypes.c_uint64)]),
+    "ghx_epochs_destroy": (c_i32, [c_vp]),
 }
 EXPORTED = tuple(_SIGS)
 

@@ -14,17 +14,25 @@ Usage mirrors the reference:
     bco.init()                                    # exchanges IPC handles (collective)
     bco.exchange().wait()                         # collective
 
-Epochs (the reference's access guards, rma/access_guard.hpp): exchange() first drains the
-caller's stream (this rank's halos are no longer read by its own kernels) and enters a barrier —
-every target is open; then it launches the puts, drains them and enters a second barrier — every
-halo of every rank has been written. Peers must share a host (torch.distributed ranks whose
+Epochs (the reference's access guards, rma/access_guard.hpp:35-140, and the bulk object's
+open / put-when-writable / wait sequence, bulk_communication_object.hpp:621-694), stream-ordered
+(epochs="device", the default): exchange() enqueues on the caller's stream
+  k_epoch(open)  -> this rank's halos are open to its sources (its earlier kernels are done with
+                    them); wait until each of its targets has opened its halos
+  puts           -> one k_put launch per group of <= 64 messages
+  k_epoch(close) -> signal each target that this epoch's puts are in; wait until each source's are
+over a flag block in node-shared host memory (libghx ghx_epochs_*). Nothing blocks the host;
+only the ranks a rank exchanges with synchronise with it; wait() reports a peer that never
+arrived (bounded waits, `timeout` seconds). epochs="host" keeps the round-2 form: drain the
+stream, barrier, puts, drain, barrier. Peers must share a host (torch.distributed ranks whose
 hostnames match); exchanges with off-node peers use CommunicationObject.
 """
 from __future__ import annotations
 
 import ctypes
+import os
+import secrets
 import socket
-from typing import List
 
 from . import _ghx
 
@@ -32,24 +40,47 @@ MAX_SLOTS = 64
 
 
 class BulkHandle:
+    """Handle of a bulk exchange: wait() blocks until this rank's halos are written (and raises
+    if a peer never reached the exchange); is_ready() polls."""
+
+    def __init__(self, bco=None, event=None):
+        self._bco, self._event = bco, event
+
     def wait(self):
-        pass
+        if self._event is not None:
+            self._event.synchronize()
+            self._check()
 
     def is_ready(self) -> bool:
+        if self._event is None:
+            return True
+        if not self._event.query():
+            return False
+        self._check()
         return True
 
     def progress(self):
-        pass
+        self.is_ready()
+
+    def _check(self):
+        bco, self._bco = self._bco, None
+        if bco is not None:
+            bco.check_epochs()
 
 
 class BulkCommunicationObject:
-    def __init__(self, context):
+    def __init__(self, context, epochs: str = "device", timeout: float = 30.0):
+        if epochs not in ("device", "host"):
+            raise ValueError("epochs must be 'device' (stream-ordered flags) or 'host' (barriers)")
         self.context = context
+        self.epochs = epochs
+        self.timeout = float(timeout)
         self._bis = []
         self._initialized = False
         self._puts = []       # [(handle, src_ptr_array, n_src, dst_ptr_array, n_dst)]
         self._imports = []    # IPC bases to close
         self._keep = []
+        self._ep = None       # ghx_epochs handle (epochs="device", more than one rank)
 
     # -- setup -------------------------------------------------------------------------------
     def add_field(self, bi):
@@ -80,8 +111,15 @@ class BulkCommunicationObject:
         if self._initialized:
             return
         me = self.context.rank()
+        world = self.context.size()
         groups = self._field_groups()
         mine = {"host": socket.gethostname(), "fields": []}
+        use_ep = self.epochs == "device" and world > 1
+        if use_ep and me == 0:
+            # the node-shared flag block: created before the setup all-gather, attached by the
+            # others after it, unlinked once every rank has attached
+            mine["epochs"] = f"/ghx_ep_{os.getpid()}_{secrets.token_hex(6)}"
+            self._ep = self._epochs_attach(mine["epochs"], True, world, me)
         for bi, (d, j) in zip(self._bis, groups):
             h = (ctypes.c_ubyte * 64)()
             off = ctypes.c_uint64()
@@ -96,6 +134,22 @@ class BulkCommunicationObject:
                 raise NotImplementedError(
                     f"rank {r} is on another host ({info['host']}): zero-copy puts need node-local "
                     "peers; use CommunicationObject for this exchange")
+        if use_ep:
+            if me != 0:
+                self._ep = self._epochs_attach(allr[0]["epochs"], False, world, me)
+            self.context.all_gather_object(None)  # every rank has attached
+            if me == 0:
+                _ghx.call("ghx_epochs_unlink", allr[0]["epochs"].encode())
+            # sources: ranks whose sends land in my halos; targets: ranks my sends land in
+            srcs = sorted({rr for bi in self._bis
+                           for _, rr, _, _ in bi.pattern_container.recv_halos(bi.local_index)
+                           if rr != me})
+            tgts = sorted({rr for bi in self._bis
+                           for _, rr, _, _ in bi.pattern_container.send_halos(bi.local_index)
+                           if rr != me})
+            _ghx.call("ghx_epochs_peers", self._ep, _ghx.i32_array(srcs), len(srcs),
+                      _ghx.i32_array(tgts), len(tgts))
+            self._ep_peers = (srcs, tgts)
         # target field table: (rank, domain, j) -> (rank, index in that rank's field list)
         target = {}
         for r, info in enumerate(allr):
@@ -167,6 +221,24 @@ class BulkCommunicationObject:
         self._keep.append(keep)
         self._puts.append((h, sp, len(self._bis), dp, len(dsts)))
 
+    def _epochs_attach(self, name, create, world, rank):
+        h = ctypes.c_void_p()
+        _ghx.call("ghx_epochs_create", name.encode(), 1 if create else 0, world, rank,
+                  self.timeout, ctypes.byref(h))
+        return h
+
+    def check_epochs(self):
+        """Raise if a wait of this rank's epochs timed out (a peer never reached the exchange)."""
+        if self._ep is None:
+            return
+        err = ctypes.c_int32()
+        _ghx.call("ghx_epochs_status", self._ep, ctypes.byref(err), None)
+        if err.value:
+            phase = "open (a target never opened its halos)" if err.value == 1 else \
+                "close (a source never completed its puts)"
+            raise RuntimeError(f"bulk exchange: an epoch wait timed out after {self.timeout:.0f} s "
+                               f"in the {phase} phase")
+
     # -- exchange ----------------------------------------------------------------------------
     def _barrier(self):
         dist = self.context.distributed
@@ -180,13 +252,26 @@ class BulkCommunicationObject:
         if not self._bis:
             return BulkHandle()
         stream = torch.cuda.current_stream(self._bis[0].field.device)
-        stream.synchronize()  # this rank's kernels no longer read its halos: targets open
-        self._barrier()
+        if self.epochs == "host":
+            stream.synchronize()  # this rank's kernels no longer read its halos: targets open
+            self._barrier()
+            for h, sp, ns, dp, nd in self._puts:
+                _ghx.call("ghx_put_execute", h, sp, ns, dp, nd, stream.cuda_stream)
+            stream.synchronize()  # this rank's puts have landed in peer memory
+            self._barrier()       # ... and every other rank's in ours
+            return BulkHandle()
+        s = stream.cuda_stream
+        if self._ep is not None:
+            _ghx.call("ghx_epochs_enqueue", self._ep, 0, s)
         for h, sp, ns, dp, nd in self._puts:
-            _ghx.call("ghx_put_execute", h, sp, ns, dp, nd, stream.cuda_stream)
-        stream.synchronize()  # this rank's puts have landed in peer memory
-        self._barrier()       # ... and every other rank's in ours
-        return BulkHandle()
+            _ghx.call("ghx_put_execute", h, sp, ns, dp, nd, s)
+        if self._ep is not None:
+            _ghx.call("ghx_epochs_enqueue", self._ep, 1, s)
+        ev = self.__dict__.get("_event")
+        if ev is None:
+            ev = self._event = torch.cuda.Event()
+        ev.record(stream)
+        return BulkHandle(self, ev)
 
     def bytes_per_exchange(self) -> int:
         tot = 0
@@ -202,10 +287,15 @@ class BulkCommunicationObject:
                 _ghx.lib().ghx_put_destroy(h)
             for b in self._imports:
                 _ghx.lib().ghx_ipc_close(ctypes.c_void_p(b))
+            if self._ep is not None:
+                _ghx.lib().ghx_epochs_destroy(self._ep)
         except Exception:
             pass
-        self._puts, self._imports = [], []
+        self._puts, self._imports, self._ep = [], [], None
 
 
-def make_bulk_communication_object(context) -> BulkCommunicationObject:
-    return BulkCommunicationObject(context)
+def make_bulk_communication_object(context, epochs: str = "device",
+                                   timeout: float = 30.0) -> BulkCommunicationObject:
+    """epochs="device": stream-ordered per-pair epochs (no host synchronisation); "host": the
+    drain + barrier form. timeout: seconds an epoch wait may take before wait() raises."""
+    return BulkCommunicationObject(context, epochs=epochs, timeout=timeout)

@@ -17,10 +17,17 @@
 // ranks that are threads of this process (loopback transport). Ranks on other hosts: throws
 // (their exchanges use communication_object).
 //
-// Epochs (the reference's access guards, include/ghex/rma/access_guard.hpp): exchange() first
-// drains the caller's stream (or the device) so this rank's kernels no longer touch its halos,
-// then a barrier (every target open); it launches the puts, drains them, and passes a second
-// barrier (every halo of every rank written). Barriers are transport all_gathers of nothing.
+// Epochs (the reference's access guards, include/ghex/rma/access_guard.hpp:35-140, and its
+// open / put-when-writable / wait sequence, bulk_communication_object.hpp:621-694). Ranks in
+// separate processes (one per GPU): stream-ordered device epochs (ghx_epochs_*): the object's
+// stream waits for the caller's stream, k_epoch(open) opens this rank's halos to its sources and
+// waits until its targets have opened theirs, the puts run, k_epoch(close) signals its targets
+// and waits for its sources; the caller's stream then waits for the object's stream. No host
+// synchronisation, no barrier; wait() reports a peer that never arrived. Ranks that are threads
+// of one process (loopback transport) share hardware queues, where one rank's waiting kernel
+// could hold back another rank's signalling kernel: they keep the host form — drain, barrier
+// (every target open), puts, drain, barrier (every halo written; barriers are transport
+// all_gathers of nothing).
 // Structured fields only (the reference's bulk object serves structured fields through
 // rma_range_generator; unstructured exchanges use communication_object).
 #pragma once
@@ -41,10 +48,39 @@ namespace ghex_amd
 {
 class bulk_handle
 {
+    hipEvent_t m_done = nullptr;       // the object's completion event (device epochs)
+    const ghx_epochs* m_ep = nullptr;
+
+    void check() const
+    {
+        if (!m_ep) return;
+        std::int32_t err = 0;
+        check_ghx(ghx_epochs_status(m_ep, &err, nullptr), "ghx_epochs_status");
+        if (err)
+            throw std::runtime_error(std::string("bulk exchange: an epoch wait timed out in the ") +
+                                     (err == 1 ? "open phase (a target never opened its halos)"
+                                               : "close phase (a source never completed its puts)"));
+    }
+
   public:
-    void wait() {}
-    bool is_ready() { return true; }
-    void progress() {}
+    bulk_handle() = default;
+    bulk_handle(hipEvent_t done, const ghx_epochs* ep)
+    : m_done{done}
+    , m_ep{ep}
+    {
+    }
+    void wait()
+    {
+        if (m_done) check_hip(hipEventSynchronize(m_done), "hipEventSynchronize");
+        check();
+    }
+    bool is_ready()
+    {
+        if (m_done && hipEventQuery(m_done) != hipSuccess) return false;
+        check();
+        return true;
+    }
+    void progress() { (void)is_ready(); }
 };
 
 class bulk_communication_object
@@ -75,6 +111,7 @@ class bulk_communication_object
     {
         std::string host;
         long pid;
+        std::string epochs;  // rank 0: name of the epochs flag block
         std::vector<remote_field> fields;
     };
     struct put
@@ -90,6 +127,9 @@ class bulk_communication_object
     std::vector<put> m_puts;
     std::vector<void*> m_imports;
     bool m_init = false;
+    ghx_epochs* m_ep = nullptr;        // device epochs (all peers in other processes)
+    std::string m_ep_name;             // rank 0: the flag block it created for this object
+    hipEvent_t m_after = nullptr, m_done = nullptr;
 
     static std::string hostname()
     {
@@ -127,6 +167,8 @@ class bulk_communication_object
         detail::put(out, std::int32_t(host.size()));
         out.insert(out.end(), host.begin(), host.end());
         detail::put(out, std::int64_t(getpid()));
+        detail::put(out, std::int32_t(m_ep_name.size()));
+        out.insert(out.end(), m_ep_name.begin(), m_ep_name.end());
         detail::put(out, std::int32_t(m_fields.size()));
         for (const auto& f : m_fields)
         {
@@ -162,6 +204,10 @@ class bulk_communication_object
         r.host.assign(in.data() + pos, std::size_t(hl));
         pos += std::size_t(hl);
         r.pid = long(detail::get<std::int64_t>(in, pos));
+        const auto nl = detail::get<std::int32_t>(in, pos);
+        if (nl < 0 || pos + std::size_t(nl) > in.size()) throw std::runtime_error("malformed bulk payload");
+        r.epochs.assign(in.data() + pos, std::size_t(nl));
+        pos += std::size_t(nl);
         const auto nf = detail::get<std::int32_t>(in, pos);
         for (std::int32_t i = 0; i < nf; ++i)
         {
@@ -240,8 +286,15 @@ class bulk_communication_object
         if (m_stream) (void)hipStreamSynchronize(m_stream);
         for (auto& p : m_puts) ghx_put_destroy(p.h);
         for (auto b : m_imports) ghx_ipc_close(b);
+        if (m_ep) ghx_epochs_destroy(m_ep);
+        if (m_after) (void)hipEventDestroy(m_after);
+        if (m_done) (void)hipEventDestroy(m_done);
         if (m_stream) (void)hipStreamDestroy(m_stream);
     }
+
+    // seconds an epoch wait may take before wait() throws (device epochs)
+    double epoch_timeout = 30.0;
+    bool device_epochs() const { return m_ep != nullptr; }
 
     hipStream_t stream() const { return m_stream; }
     bool initialized() const { return m_init; }
@@ -265,6 +318,16 @@ class bulk_communication_object
     {
         if (m_init) return;
         const int me = m_ctx->rank();
+        const int world = m_ctx->size();
+        if (me == 0 && world > 1)
+        {
+            // created before the all-gather so the others can attach after it (if they all live
+            // in other processes; otherwise it is dropped again below)
+            m_ep_name = "/ghx_ep_" + std::to_string(getpid()) + "_" +
+                        std::to_string(reinterpret_cast<std::uintptr_t>(this) & 0xffffffu);
+            check_ghx(ghx_epochs_create(m_ep_name.c_str(), 1, world, 0, epoch_timeout, &m_ep),
+                      "ghx_epochs_create");
+        }
         const auto gathered = m_ctx->get_transport().all_gather(serialize_mine());
         std::vector<remote_rank> all;
         for (const auto& g : gathered) all.push_back(deserialize(g));
@@ -273,6 +336,41 @@ class bulk_communication_object
             if (all[r].host != mine.host)
                 throw std::runtime_error("rank " + std::to_string(r) + " is on another host (" + all[r].host +
                                          "): zero-copy puts need node-local peers; use communication_object");
+        bool distinct = world > 1;  // every rank its own process: device epochs
+        for (std::size_t r = 0; r < all.size() && distinct; ++r)
+            for (std::size_t q = 0; q < r && distinct; ++q) distinct = all[r].pid != all[q].pid;
+        if (distinct && me != 0)
+            check_ghx(ghx_epochs_create(all[0].epochs.c_str(), 0, world, me, epoch_timeout, &m_ep),
+                      "ghx_epochs_create");
+        if (world > 1) barrier();  // every rank attached (or decided not to)
+        if (me == 0 && world > 1)
+        {
+            (void)ghx_epochs_unlink(m_ep_name.c_str());
+            if (!distinct)
+            {
+                ghx_epochs_destroy(m_ep);
+                m_ep = nullptr;
+            }
+        }
+        if (m_ep)
+        {
+            std::vector<std::int32_t> srcs, tgts;
+            for (const auto& f : m_fields)
+                for (int dir = 0; dir < 2; ++dir)
+                    for (const auto& h : halos(*f.pattern, f.local_index, dir))
+                    {
+                        const int rr = std::get<1>(h);
+                        auto& v = dir == 0 ? tgts : srcs;
+                        if (rr != me && std::find(v.begin(), v.end(), rr) == v.end()) v.push_back(rr);
+                    }
+            std::sort(srcs.begin(), srcs.end());
+            std::sort(tgts.begin(), tgts.end());
+            check_ghx(ghx_epochs_peers(m_ep, srcs.data(), std::int32_t(srcs.size()), tgts.data(),
+                                       std::int32_t(tgts.size())),
+                      "ghx_epochs_peers");
+            check_hip(hipEventCreateWithFlags(&m_after, hipEventDisableTiming), "hipEventCreate");
+            check_hip(hipEventCreateWithFlags(&m_done, hipEventDisableTiming), "hipEventCreate");
+        }
         std::map<std::tuple<int, int, int>, std::pair<int, int>> target;  // (rank, domain, j)
         for (std::size_t r = 0; r < all.size(); ++r)
             for (std::size_t i = 0; i < all[r].fields.size(); ++i)
@@ -343,6 +441,26 @@ class bulk_communication_object
     bulk_handle exchange(hipStream_t after = nullptr)
     {
         if (!m_init) init();
+        if (m_ep)
+        {
+            // stream-ordered: the object's stream follows `after` (or the device), the epochs
+            // and puts run on it, and `after` follows it again
+            if (after)
+            {
+                check_hip(hipEventRecord(m_after, after), "hipEventRecord");
+                check_hip(hipStreamWaitEvent(m_stream, m_after, 0), "hipStreamWaitEvent");
+            }
+            else check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            check_ghx(ghx_epochs_enqueue(m_ep, 0, m_stream), "ghx_epochs_enqueue(open)");
+            for (auto& p : m_puts)
+                check_ghx(ghx_put_execute(p.h, m_src.data(), std::int32_t(m_src.size()), p.dst.data(),
+                                          std::int32_t(p.dst.size()), m_stream),
+                          "ghx_put_execute");
+            check_ghx(ghx_epochs_enqueue(m_ep, 1, m_stream), "ghx_epochs_enqueue(close)");
+            check_hip(hipEventRecord(m_done, m_stream), "hipEventRecord");
+            if (after) check_hip(hipStreamWaitEvent(after, m_done, 0), "hipStreamWaitEvent");
+            return {m_done, m_ep};
+        }
         if (after) check_hip(hipStreamSynchronize(after), "hipStreamSynchronize");
         else check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
         barrier();  // every target open

@@ -9,7 +9,7 @@ its send regions straight into the peers' fields through IPC mappings (same GPU 
 GPUs over xGMI on a multi-GPU node). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk|sched|pipe]"""
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk|bulkhost|bulkrace|sched|pipe]"""
 import os
 import sys
 
@@ -44,11 +44,32 @@ def main():
         expect = H.expected_linear_halo(a, dom, N, Hw, gl, layout=layout)
         base, logical = device_field(a, layout)
         fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)
-        if mode == "bulk":
-            co = ghex_amd.make_bulk_communication_object(ctx)
+        if mode in ("bulk", "bulkhost"):
+            co = ghex_amd.make_bulk_communication_object(
+                ctx, epochs="host" if mode == "bulkhost" else "device", timeout=60)
             co.add_field(pc(fd))
             for _ in range(reps):
                 co.exchange().wait()
+        elif mode == "bulkrace":
+            # device epochs only order the exchanges: per exchange k, on the stream and with no
+            # host synchronisation, the field is rewritten (owned cells x f_k, halos -f_k), the
+            # exchange runs, and the halos are compared with the expected values x f_k into a
+            # device counter. A put that landed before its target opened, or a halo read before
+            # every source finished, would leave cells of another epoch behind.
+            co = ghex_amd.make_bulk_communication_object(ctx, timeout=60)
+            co.add_field(pc(fd))
+            src = torch.from_numpy(a).cuda()
+            exp_d = torch.from_numpy(expect).cuda()
+            nbad = torch.zeros((), dtype=torch.int64, device="cuda")
+            h = None
+            for k in range(4 * reps):
+                f = float(k % 5 + 1)
+                base.copy_(src * f)
+                h = co.exchange()
+                nbad += (base != exp_d * f).sum()
+            h.wait()
+            bad += int(nbad.item())
+            continue
         elif mode == "sched":  # schedule_exchange on a side stream, host-staged transport
             co = R.make_communication_object(ctx, staging="host")
             s = torch.cuda.Stream()

@@ -244,3 +244,31 @@ def test_put_plan_pairs_matching_sides_and_refuses_mismatch():
     (a, ka), (b, kb) = _put_entries([(3, 1, 1), (1, 3, 1)])
     assert L.ghx_put_create(ctypes.byref(a), 1, ctypes.byref(b), 1, ctypes.byref(h)) == -1
     assert b"same message bytes" in L.ghx_last_error()
+
+
+def test_epochs_flag_block_argument_checks_and_cleanup(ghx):
+    """ghx_epochs_* (device-side access epochs of the bulk exchange) without a GPU: bad names,
+    world/rank and timeouts are refused; a creating rank that cannot register the block (no
+    device here) leaves no shared-memory segment behind; attaching to a missing block fails."""
+    import ctypes
+    import os
+    L = ghx.lib()
+    h = ctypes.c_void_p()
+    assert L.ghx_epochs_create(b"no-slash", 1, 2, 0, 1.0, ctypes.byref(h)) == -1
+    assert L.ghx_epochs_create(b"/a/b", 1, 2, 0, 1.0, ctypes.byref(h)) == -1
+    assert L.ghx_epochs_create(b"/ghx_t", 1, 65, 0, 1.0, ctypes.byref(h)) == -1
+    assert L.ghx_epochs_create(b"/ghx_t", 1, 2, 2, 1.0, ctypes.byref(h)) == -1
+    assert L.ghx_epochs_create(b"/ghx_t", 1, 2, 0, 0.0, ctypes.byref(h)) == -1
+    name = f"/ghx_test_{os.getpid()}"
+    rc = L.ghx_epochs_create(name.encode(), 1, 2, 0, 1.0, ctypes.byref(h))
+    if rc == 0:  # a GPU is present: clean up and stop here
+        L.ghx_epochs_unlink(name.encode())
+        L.ghx_epochs_destroy(h)
+        return
+    assert rc == -2 and b"hipHostRegister" in L.ghx_last_error()
+    assert not os.path.exists("/dev/shm" + name)
+    assert L.ghx_epochs_create(name.encode(), 0, 2, 1, 1.0, ctypes.byref(h)) == -1
+    assert b"shm_open" in L.ghx_last_error()
+    assert L.ghx_epochs_unlink(name.encode()) == -1
+    assert L.ghx_epochs_peers(None, None, 0, None, 0) == -1
+    assert L.ghx_epochs_enqueue(None, 0, None) == -1
