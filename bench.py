@@ -656,7 +656,11 @@ def extras(args, torch, dist, dev, stream, out, v):
             bco.init()
             for _ in range(3):
                 bco.exchange().wait()
-            Tb = timed(lambda: bco.exchange().wait(), ke)
+            # stream-ordered (device epochs): K exchanges back to back, one host sync at the end;
+            # and with a host wait after every exchange (what a caller that blocks pays)
+            Tb = timed(lambda: bco.exchange(), ke)
+            bco.check_epochs()
+            Tbw = timed(lambda: bco.exchange().wait(), ke)
             put = bco._puts[0]
 
             def put_fn(s):
@@ -665,6 +669,8 @@ def extras(args, torch, dist, dev, stream, out, v):
                     raise RuntimeError(L.ghx_last_error().decode())
             (t_put,) = kernel_durations(torch, dev, stream, [put_fn])
             out["bulk"] = {"exchange_ms_per_step": round(Tb / ke * 1e3, 4),
+                           "exchange_wait_ms_per_step": round(Tbw / ke * 1e3, 4),
+                           "epochs": bco.epochs,
                            "put_launches": len(bco._puts),
                            "put_us": round(t_put * 1e6, 2) if len(bco._puts) == 1 else None,
                            "bytes_moved_per_step": 2 * n_halo * 8}

@@ -267,6 +267,8 @@ class BulkCommunicationObject:
             _ghx.call("ghx_put_execute", h, sp, ns, dp, nd, s)
         if self._ep is not None:
             _ghx.call("ghx_epochs_enqueue", self._ep, 1, s)
+        if torch.cuda.is_current_stream_capturing():
+            return BulkHandle(self, None)  # captured into a graph: completion is the replay's
         ev = self.__dict__.get("_event")
         if ev is None:
             ev = self._event = torch.cuda.Event()

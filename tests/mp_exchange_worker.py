@@ -9,7 +9,7 @@ its send regions straight into the peers' fields through IPC mappings (same GPU 
 GPUs over xGMI on a multi-GPU node). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk|bulkhost|bulkrace|sched|pipe]"""
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk|bulkhost|bulkrace|bulkgraph|sched|pipe]"""
 import os
 import sys
 
@@ -68,6 +68,32 @@ def main():
                 h = co.exchange()
                 nbad += (base != exp_d * f).sum()
             h.wait()
+            bad += int(nbad.item())
+            continue
+        elif mode == "bulkgraph":
+            # the whole bulk exchange (epoch open, puts, epoch close) captured once into a graph
+            # and replayed: the epoch counters live in memory, so every replay is a new epoch
+            co = ghex_amd.make_bulk_communication_object(ctx, timeout=60)
+            co.add_field(pc(fd))
+            co.exchange().wait()
+            src = torch.from_numpy(a).cuda()
+            exp_d = torch.from_numpy(expect).cuda()
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                co.exchange()
+            torch.cuda.current_stream().wait_stream(side)
+            with torch.cuda.graph(g):
+                co.exchange()
+            nbad = torch.zeros((), dtype=torch.int64, device="cuda")
+            for k in range(3 * reps):
+                f = float(k % 5 + 1)
+                base.copy_(src * f)
+                g.replay()
+                nbad += (base != exp_d * f).sum()
+            torch.cuda.synchronize()
+            co.check_epochs()
             bad += int(nbad.item())
             continue
         elif mode == "sched":  # schedule_exchange on a side stream, host-staged transport
