@@ -173,9 +173,14 @@ class CommunicationObject:
     """communication_object<grid, domain_id> (make_communication_object, :1105-1112)."""
 
     def __init__(self, context, fuse_self: bool = True, staging=None, pipelined: bool = False,
-                 rccl_self: bool = False, max_streams: int = 4):
+                 rccl_self: bool = False, max_streams: int = 4, copy_engine: str = "probe"):
         if staging not in (None, "host"):
             raise ValueError("staging must be None (device buffers) or 'host'")
+        if copy_engine not in ("probe", "runtime"):
+            raise ValueError("copy_engine must be 'probe' (measured SDMA engines) or 'runtime'")
+        # host staging: "probe" = D2H / H2D on the SDMA engines ghex_amd.staging measured,
+        # "runtime" = hipMemcpyAsync (the HIP runtime picks the engines)
+        self.copy_engine = copy_engine
         if rccl_self and staging == "host":
             # the host-staged pipeline keeps self messages on the device (recv aliases send);
             # routing them through RCCL is a device-buffer-only test mode
@@ -406,10 +411,43 @@ class CommunicationObject:
         return h
 
     def _exchange_host_staged(self, plan, sends, recvs, stream):
-        """pack (queued) -> per-buffer D2H + event -> host sends as copies land; host recvs ->
-        per-buffer H2D as messages land; the caller queues the unpack behind the H2D copies."""
+        """pack (queued) -> D2H per buffer -> host sends as copies land; host recvs -> H2D per
+        buffer as messages land; the caller queues the unpack afterwards. copy_engine="probe":
+        copies on the measured SDMA engines (the host waits for the pack, the copy engines run
+        D2H and H2D concurrently; the unpack is queued behind an L2 acquire); "runtime": the
+        copies are hipMemcpyAsync on the exchange stream."""
         import torch
         hs, hr = self._host_buffers(plan, sends, recvs)
+        dist = self.context.distributed
+        group = self._host_group
+        gr = self.context.global_rank
+        if self.copy_engine == "probe":
+            from .staging import Copier
+            cp = Copier.for_device(stream.device)
+            packed = torch.cuda.Event()
+            packed.record(stream)
+            rops = [(dist.irecv(h, gr(peer), group, tag), h, peer, tag)
+                    for (peer, tag, _), h in sorted(zip(recvs, hr), key=lambda x: (x[0][0], x[0][1]))]
+            packed.synchronize()  # the send buffers are complete
+            tks = [cp.d2h(h.data_ptr(), t.data_ptr(), t.numel()) for (_, _, t), h in zip(sends, hs)]
+            sops = []
+            for ((peer, tag, _), h), tk in sorted(zip(zip(sends, hs), tks),
+                                                  key=lambda x: (x[0][0][0], x[0][0][1])):
+                cp.wait(tk)
+                sops.append(dist.isend(h, gr(peer), group, tag))
+            dev_of = {(p, g): t for p, g, t in recvs}
+            h2d = []
+            for w, h, peer, tag in rops:
+                w.wait()
+                t = dev_of[(peer, tag)]
+                h2d.append(cp.h2d(t.data_ptr(), h.data_ptr(), t.numel()))
+            for tk in h2d:
+                cp.wait(tk)
+            if h2d:
+                cp.acquire(stream)
+            for w in sops:
+                w.wait()
+            return
         evs = []
         with torch.cuda.stream(stream):
             for (_, _, t), h in zip(sends, hs):
@@ -417,16 +455,14 @@ class CommunicationObject:
                 ev = torch.cuda.Event()
                 ev.record(stream)
                 evs.append(ev)
-        dist = self.context.distributed
-        group = self._host_group
         rops = []
         for (peer, tag, _), h in sorted(zip(recvs, hr), key=lambda x: (x[0][0], x[0][1])):
-            rops.append((dist.irecv(h, self.context.global_rank(peer), group, tag), h, peer, tag))
+            rops.append((dist.irecv(h, gr(peer), group, tag), h, peer, tag))
         sops = []
         for ((peer, tag, _), h), ev in sorted(zip(zip(sends, hs), evs),
                                               key=lambda x: (x[0][0][0], x[0][0][1])):
             ev.synchronize()
-            sops.append(dist.isend(h, self.context.global_rank(peer), group, tag))
+            sops.append(dist.isend(h, gr(peer), group, tag))
         dev_of = {(p, g): t for p, g, t in recvs}
         with torch.cuda.stream(stream):
             for w, h, peer, tag in rops:
@@ -496,6 +532,10 @@ class CommunicationObject:
         start = torch.cuda.Event()
         start.record(stream)
         landed = {}
+        probe = self.copy_engine == "probe"
+        if probe:
+            from .staging import Copier
+            cp = Copier.for_device(device)
         lane_of = {p: k % self.max_streams for k, p in enumerate(peers)}
         for p in peers:
             sp = self._peer_stream(lane_of[p], device)
@@ -503,9 +543,10 @@ class CommunicationObject:
             for i in sends_of.get(p, []):
                 _ghx.check(L.ghx_exchange_pack_buffer(plan.h, i, fptrs, nf, sptrs, len(send),
                                                       sp.cuda_stream), "pack_buffer")
-                with torch.cuda.stream(sp):
-                    hs[i][:plan.send[i]["size"]].copy_(send[i][:plan.send[i]["size"]],
-                                                       non_blocking=True)
+                if not probe:
+                    with torch.cuda.stream(sp):
+                        hs[i][:plan.send[i]["size"]].copy_(send[i][:plan.send[i]["size"]],
+                                                           non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(sp)
             landed[p] = ev
@@ -528,9 +569,15 @@ class CommunicationObject:
                                         x["tag"]), j, p])
         sops = []
         for p in peers:
-            landed[p].synchronize()
-            for i in sorted(sends_of.get(p, []), key=lambda i: (plan.send[i]["tag"], plan.send[i]["pair"])):
+            landed[p].synchronize()  # this peer's packs (and, with "runtime" copies, its D2H)
+            order = sorted(sends_of.get(p, []), key=lambda i: (plan.send[i]["tag"], plan.send[i]["pair"]))
+            if probe:
+                tks = {i: cp.d2h(hs[i].data_ptr(), send[i].data_ptr(), plan.send[i]["size"])
+                       for i in order if plan.send[i]["size"]}
+            for i in order:
                 x = plan.send[i]
+                if probe and i in tks:
+                    cp.wait(tks[i])
                 sops.append(dist.isend(hs[i][:x["size"]], self.context.global_rank(p), group,
                                        x["tag"]))
         # every send is posted before the first blocking receive wait, so the in-order waits
@@ -540,8 +587,13 @@ class CommunicationObject:
             w.wait()
             sp = self._peer_stream(lane_of[p], device)
             n = plan.recv[j]["size"]
-            with torch.cuda.stream(sp):
-                recv[j][:n].copy_(hr[j][:n], non_blocking=True)
+            if probe:
+                if n:
+                    cp.wait(cp.h2d(recv[j].data_ptr(), hr[j].data_ptr(), n))
+                    cp.acquire(sp)
+            else:
+                with torch.cuda.stream(sp):
+                    recv[j][:n].copy_(hr[j][:n], non_blocking=True)
             _ghx.check(L.ghx_exchange_unpack_buffer(plan.h, j, fptrs, nf, rptrs, len(recv),
                                                     sp.cuda_stream), "unpack_buffer")
         for w in sops:

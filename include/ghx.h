@@ -442,6 +442,31 @@ int ghx_epochs_enqueue(const ghx_epochs* ep, int32_t phase, ghx_stream stream);
 int ghx_epochs_status(const ghx_epochs* ep, int32_t* error, uint64_t* epoch);
 int ghx_epochs_destroy(ghx_epochs* ep);
 
+/* ------------------------------------------------------------------------------------------
+ * Host staging copies (the NIC-side path): device <-> pinned host copies on
+ * SDMA engines chosen by measurement. Replaces the staging the reference leaves to its transport
+ * (oomph device/host buffers, include/ghex/arch_traits.hpp:51-75; the non-stream-aware branch of
+ * include/ghex/communication_object.hpp:611-637, 715-729). hipMemcpyAsync lets the runtime pick
+ * the engine, and D2H and H2D of one exchange often end up on one engine (serialised) or on a
+ * slow one; ghx_copier_create probes engines 0-3 with `probe_bytes` copies per direction and
+ * alone / concurrently, and keeps the pair (D2H engine, H2D engine) with the best concurrent
+ * rate (ghx_copier_info). ghx_copier_submit enqueues one copy (direction 0 = device -> host,
+ * 1 = host -> device; host memory must be pinned, e.g. hipHostMalloc) and returns a ticket; with
+ * after_ticket >= 0 the copy engine starts it only once that earlier copy has completed (no host
+ * round trip). ghx_copier_wait blocks until a ticket's copy has completed (error after
+ * `timeout_s`). ghx_copier_acquire enqueues, on a stream, the cache invalidation that kernels
+ * reading bytes an H2D copy has written need before them (the HIP runtime does not see these
+ * copies, so it would not add it). Not thread-safe: one copier per thread. */
+typedef struct ghx_copier ghx_copier;
+int ghx_copier_create(uint64_t probe_bytes, double timeout_s, ghx_copier** out);
+int ghx_copier_info(const ghx_copier* c, int32_t* d2h_engine, int32_t* h2d_engine, float* d2h_GBps,
+                    float* h2d_GBps, float* both_GBps);
+int ghx_copier_submit(ghx_copier* c, void* dst, const void* src, uint64_t bytes, int32_t direction,
+                      int64_t after_ticket, uint64_t* ticket);
+int ghx_copier_wait(ghx_copier* c, uint64_t ticket);
+int ghx_copier_acquire(const ghx_copier* c, ghx_stream stream);
+int ghx_copier_destroy(ghx_copier* c);
+
 #ifdef __cplusplus
 }
 #endif

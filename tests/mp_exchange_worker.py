@@ -9,7 +9,7 @@ its send regions straight into the peers' fields through IPC mappings (same GPU 
 GPUs over xGMI on a multi-GPU node). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|bulk|bulkhost|bulkrace|bulkgraph|sched|pipe]"""
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkrace|bulkgraph|sched|pipe|pipert]"""
 import os
 import sys
 
@@ -106,6 +106,15 @@ def main():
                 h.wait()
         elif mode == "pipe":  # per-peer streams: pack -> D2H -> send as landed -> H2D -> unpack
             co = R.make_communication_object(ctx, staging="host", pipelined=True)
+            for _ in range(reps):
+                co.exchange([pc(fd)]).wait()
+        elif mode == "stagedrt":  # host staging with hipMemcpyAsync (runtime-chosen engines)
+            co = R.make_communication_object(ctx, staging="host", copy_engine="runtime")
+            for _ in range(reps):
+                co.exchange([pc(fd)]).wait()
+        elif mode == "pipert":
+            co = R.make_communication_object(ctx, staging="host", pipelined=True,
+                                             copy_engine="runtime")
             for _ in range(reps):
                 co.exchange([pc(fd)]).wait()
         else:
