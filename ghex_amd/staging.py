@@ -13,10 +13,12 @@ after `acquire(stream)`, which invalidates the L2 caches on that stream first.""
 from __future__ import annotations
 
 import ctypes
+import threading
 
 from . import _ghx
 
 _copiers = {}
+_lock = threading.Lock()
 
 
 class Copier:
@@ -27,15 +29,17 @@ class Copier:
         with torch.cuda.device(self.device):
             _ghx.call("ghx_copier_create", probe_bytes, float(timeout), ctypes.byref(h))
         self.h = h
+        self._lock = threading.Lock()  # the native copier is not thread-safe
 
     @classmethod
     def for_device(cls, device) -> "Copier":
         """The process's copier for `device` (probed at the first request)."""
         import torch
         key = torch.device(device).index or 0
-        c = _copiers.get(key)
-        if c is None:
-            c = _copiers[key] = cls(torch.device("cuda", key))
+        with _lock:
+            c = _copiers.get(key)
+            if c is None:
+                c = _copiers[key] = cls(torch.device("cuda", key))
         return c
 
     def info(self) -> dict:
@@ -48,8 +52,9 @@ class Copier:
 
     def _submit(self, dst, src, nbytes, direction, after):
         t = ctypes.c_uint64()
-        _ghx.call("ghx_copier_submit", self.h, ctypes.c_void_p(dst), ctypes.c_void_p(src),
-                  int(nbytes), direction, -1 if after is None else int(after), ctypes.byref(t))
+        with self._lock:
+            _ghx.call("ghx_copier_submit", self.h, ctypes.c_void_p(dst), ctypes.c_void_p(src),
+                      int(nbytes), direction, -1 if after is None else int(after), ctypes.byref(t))
         return t.value
 
     def d2h(self, host_ptr, dev_ptr, nbytes, after=None) -> int:
@@ -62,7 +67,8 @@ class Copier:
         return self._submit(dev_ptr, host_ptr, nbytes, 1, after)
 
     def wait(self, ticket: int):
-        _ghx.call("ghx_copier_wait", self.h, int(ticket))
+        with self._lock:
+            _ghx.call("ghx_copier_wait", self.h, int(ticket))
 
     def acquire(self, stream):
         """Enqueue the L2 invalidation kernels reading H2D-copied bytes need before them."""
