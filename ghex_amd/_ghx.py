@@ -77,6 +77,7 @@ _SIGS = {
                                                 P(c_i64), P(c_i64), P(c_i64), P(c_i64), c_i32,
                                                 P(c_vp)]),
     "ghx_pattern_destroy": (c_i32, [c_vp]),
+    "ghx_pattern_filter": (c_i32, [c_vp, P(c_i32), c_i32, c_i32, P(c_vp)]),
     "ghx_pattern_num_domains": (c_i32, [c_vp, P(c_i32)]),
     "ghx_pattern_max_tag": (c_i32, [c_vp, P(c_i32)]),
     "ghx_pattern_domain_id": (c_i32, [c_vp, c_i32, P(c_i32)]),

@@ -24,8 +24,11 @@ open / put-when-writable / wait sequence, bulk_communication_object.hpp:621-694)
 over a flag block in node-shared host memory (libghx ghx_epochs_*). Nothing blocks the host;
 only the ranks a rank exchanges with synchronise with it; wait() reports a peer that never
 arrived (bounded waits, `timeout` seconds). epochs="host" keeps the round-2 form: drain the
-stream, barrier, puts, drain, barrier. Peers must share a host (torch.distributed ranks whose
-hostnames match); exchanges with off-node peers use CommunicationObject.
+stream, barrier, puts, drain, barrier. Puts go to node-local peers (ranks whose hostnames
+match); the halos of ranks on other hosts travel through a CommunicationObject over the
+pattern's remote part (`remote_options`), started in the same exchange() and awaited by the same
+wait() — the reference's local / remote pattern maps and its m_co
+(bulk_communication_object.hpp:330-383, 674-694).
 """
 from __future__ import annotations
 
@@ -39,19 +42,32 @@ from . import _ghx
 MAX_SLOTS = 64
 
 
+def hostname() -> str:
+    """This rank's host as the bulk exchange groups ranks (GHX_HOSTNAME overrides it: tests emulate
+    several hosts on one machine)."""
+    return os.environ.get("GHX_HOSTNAME") or socket.gethostname()
+
+
 class BulkHandle:
     """Handle of a bulk exchange: wait() blocks until this rank's halos are written (and raises
     if a peer never reached the exchange); is_ready() polls."""
 
-    def __init__(self, bco=None, event=None):
-        self._bco, self._event = bco, event
+    def __init__(self, bco=None, event=None, remote=None):
+        self._bco, self._event, self._remote = bco, event, remote
 
     def wait(self):
+        if self._remote is not None:
+            self._remote.wait()
+            self._remote = None
         if self._event is not None:
             self._event.synchronize()
             self._check()
 
     def is_ready(self) -> bool:
+        if self._remote is not None:
+            if not self._remote.is_ready():
+                return False
+            self._remote = None
         if self._event is None:
             return True
         if not self._event.query():
@@ -69,12 +85,16 @@ class BulkHandle:
 
 
 class BulkCommunicationObject:
-    def __init__(self, context, epochs: str = "device", timeout: float = 30.0):
+    def __init__(self, context, epochs: str = "device", timeout: float = 30.0,
+                 remote_options=None):
         if epochs not in ("device", "host"):
             raise ValueError("epochs must be 'device' (stream-ordered flags) or 'host' (barriers)")
         self.context = context
         self.epochs = epochs
         self.timeout = float(timeout)
+        # options of the buffered CommunicationObject that carries halos to/from other hosts
+        self.remote_options = dict(remote_options or {})
+        self._co, self._remote_bis = None, []
         self._bis = []
         self._initialized = False
         self._puts = []       # [(handle, src_ptr_array, n_src, dst_ptr_array, n_dst)]
@@ -113,13 +133,8 @@ class BulkCommunicationObject:
         me = self.context.rank()
         world = self.context.size()
         groups = self._field_groups()
-        mine = {"host": socket.gethostname(), "fields": []}
-        use_ep = self.epochs == "device" and world > 1
-        if use_ep and me == 0:
-            # the node-shared flag block: created before the setup all-gather, attached by the
-            # others after it, unlinked once every rank has attached
-            mine["epochs"] = f"/ghx_ep_{os.getpid()}_{secrets.token_hex(6)}"
-            self._ep = self._epochs_attach(mine["epochs"], True, world, me)
+        host = hostname()
+        mine = {"host": host, "fields": []}
         for bi, (d, j) in zip(self._bis, groups):
             h = (ctypes.c_ubyte * 64)()
             off = ctypes.c_uint64()
@@ -129,24 +144,40 @@ class BulkCommunicationObject:
             mine["fields"].append({"domain": d, "j": j, "desc": bytes(bi.field.desc),
                                    "ipc": bytes(h), "offset": off.value, "recv": recv})
         allr = self.context.all_gather_object(mine)
-        for r, info in enumerate(allr):
-            if info["host"] != mine["host"]:
-                raise NotImplementedError(
-                    f"rank {r} is on another host ({info['host']}): zero-copy puts need node-local "
-                    "peers; use CommunicationObject for this exchange")
-        if use_ep:
-            if me != 0:
-                self._ep = self._epochs_attach(allr[0]["epochs"], False, world, me)
+        local = sorted(r for r, info in enumerate(allr) if info["host"] == host)
+        remote = [r for r in range(world) if r not in local]
+        if remote:
+            # ranks on other hosts: their halos travel through a buffered exchange of the
+            # pattern's remote part (the reference's remote pattern map + m_co,
+            # bulk_communication_object.hpp:330-383, 674-694); node-local ones are put
+            from .communication_object import CommunicationObject
+            part = {}
+            for bi in self._bis:
+                pc = bi.pattern_container
+                if id(pc) not in part:
+                    part[id(pc)] = pc.filtered(remote, keep=True)
+            self._remote_bis = [part[id(bi.pattern_container)](bi.field) for bi in self._bis]
+            self._co = CommunicationObject(self.context, **self.remote_options)
+        if self.epochs == "device" and world > 1:
+            # one node-shared flag block per host: created by the host's lowest rank, attached by
+            # the others after an all-gather of the names, unlinked once all have attached
+            leader = local[0]
+            name = f"/ghx_ep_{os.getpid()}_{secrets.token_hex(6)}" if me == leader else None
+            if me == leader:
+                self._ep = self._epochs_attach(name, True, world, me)
+            names = self.context.all_gather_object(name)
+            if me != leader:
+                self._ep = self._epochs_attach(names[leader], False, world, me)
             self.context.all_gather_object(None)  # every rank has attached
-            if me == 0:
-                _ghx.call("ghx_epochs_unlink", allr[0]["epochs"].encode())
-            # sources: ranks whose sends land in my halos; targets: ranks my sends land in
+            if me == leader:
+                _ghx.call("ghx_epochs_unlink", name.encode())
+            # sources: node-local ranks whose puts land in my halos; targets: those mine land in
             srcs = sorted({rr for bi in self._bis
                            for _, rr, _, _ in bi.pattern_container.recv_halos(bi.local_index)
-                           if rr != me})
+                           if rr != me and rr in local})
             tgts = sorted({rr for bi in self._bis
                            for _, rr, _, _ in bi.pattern_container.send_halos(bi.local_index)
-                           if rr != me})
+                           if rr != me and rr in local})
             _ghx.call("ghx_epochs_peers", self._ep, _ghx.i32_array(srcs), len(srcs),
                       _ghx.i32_array(tgts), len(tgts))
             self._ep_peers = (srcs, tgts)
@@ -159,6 +190,8 @@ class BulkCommunicationObject:
         msgs = []
         for k, (bi, (d, j)) in enumerate(zip(self._bis, groups)):
             for rid, rr, tag, spaces in bi.pattern_container.send_halos(bi.local_index):
+                if rr not in local:
+                    continue  # a remote rank: the buffered exchange carries it
                 key = (rr, rid, j)
                 if key not in target:
                     raise RuntimeError(f"rank {rr} registered no field #{j} for domain {rid}")
@@ -252,6 +285,7 @@ class BulkCommunicationObject:
         if not self._bis:
             return BulkHandle()
         stream = torch.cuda.current_stream(self._bis[0].field.device)
+        remote = self._co.exchange(self._remote_bis) if self._co is not None else None
         if self.epochs == "host":
             stream.synchronize()  # this rank's kernels no longer read its halos: targets open
             self._barrier()
@@ -259,7 +293,7 @@ class BulkCommunicationObject:
                 _ghx.call("ghx_put_execute", h, sp, ns, dp, nd, stream.cuda_stream)
             stream.synchronize()  # this rank's puts have landed in peer memory
             self._barrier()       # ... and every other rank's in ours
-            return BulkHandle()
+            return BulkHandle(remote=remote)
         s = stream.cuda_stream
         if self._ep is not None:
             _ghx.call("ghx_epochs_enqueue", self._ep, 0, s)
@@ -273,7 +307,7 @@ class BulkCommunicationObject:
         if ev is None:
             ev = self._event = torch.cuda.Event()
         ev.record(stream)
-        return BulkHandle(self, ev)
+        return BulkHandle(self, ev, remote)
 
     def bytes_per_exchange(self) -> int:
         tot = 0
@@ -296,8 +330,11 @@ class BulkCommunicationObject:
         self._puts, self._imports, self._ep = [], [], None
 
 
-def make_bulk_communication_object(context, epochs: str = "device",
-                                   timeout: float = 30.0) -> BulkCommunicationObject:
+def make_bulk_communication_object(context, epochs: str = "device", timeout: float = 30.0,
+                                   remote_options=None) -> BulkCommunicationObject:
     """epochs="device": stream-ordered per-pair epochs (no host synchronisation); "host": the
-    drain + barrier form. timeout: seconds an epoch wait may take before wait() raises."""
-    return BulkCommunicationObject(context, epochs=epochs, timeout=timeout)
+    drain + barrier form. timeout: seconds an epoch wait may take before wait() raises.
+    remote_options: CommunicationObject options for the halos of ranks on other hosts (e.g.
+    staging="host"); node-local ranks always get puts."""
+    return BulkCommunicationObject(context, epochs=epochs, timeout=timeout,
+                                   remote_options=remote_options)

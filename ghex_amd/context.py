@@ -66,7 +66,9 @@ class Context:
                 buf = (ctypes.c_ubyte * 128)()
                 _ghx.call("ghx_rccl_unique_id", buf)
                 mine[(me, p)] = bytes(buf)
-        every = self.all_gather_object(mine) if want else []
+        # collective on every call, also when this rank needs no new communicator: another rank
+        # may (the call happens at the same point of every rank's program)
+        every = self.all_gather_object(mine)
         for p in order(want):
             a, b = min(me, p), max(me, p)
             uid = every[a].get((a, b))  # drawn by the lower rank of the pair

@@ -812,6 +812,34 @@ int ghx_unstructured_pattern_create(int32_t n_domains, const int32_t* domain_ids
     });
 }
 
+int ghx_pattern_filter(const ghx_pattern* p, const int32_t* ranks, int32_t n_ranks, int32_t keep,
+                       ghx_pattern** out)
+{
+    return guarded([&] {
+        check_ptr(p, "pattern");
+        check_ptr(out, "out");
+        if (n_ranks < 0 || (n_ranks > 0 && !ranks)) throw invalid("bad rank list");
+        if (keep != 0 && keep != 1) throw invalid("keep must be 0 or 1");
+        auto in_set = [&](int32_t r) {
+            for (int32_t i = 0; i < n_ranks; ++i)
+                if (ranks[i] == r) return true;
+            return false;
+        };
+        auto q = std::make_unique<ghx_pattern>();
+        static_cast<pattern_set&>(*q) = static_cast<const pattern_set&>(*p);
+        for (auto& d : q->doms)
+            for (auto* v : {&d.send, &d.recv})
+            {
+                std::vector<halo_entry> kept;
+                for (auto& e : *v)
+                    if (in_set(e.key.remote_rank) == (keep == 1)) kept.push_back(std::move(e));
+                v->swap(kept);
+            }
+        *out = q.release();
+        return GHX_OK;
+    });
+}
+
 int ghx_pattern_destroy(ghx_pattern* p)
 {
     return guarded([&] {

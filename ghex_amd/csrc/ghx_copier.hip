@@ -225,17 +225,39 @@ int ghx_copier_create(uint64_t probe_bytes, double timeout_s, ghx_copier** out)
         std::memset(h, 0, 2 * n);
         try
         {
+            // the status masks say which engines are idle at this instant (another process may
+            // be copying); a busy engine still serves copies, so every engine 0-3 is probed and
+            // only one that refuses a copy is left out
+            (void)m_d2h;
+            (void)m_h2d;
             double best[2][kProbeEngines];
             for (int dir = 0; dir < 2; ++dir)
                 for (int e = 0; e < kProbeEngines; ++e)
-                    best[dir][e] = (((dir ? m_h2d : m_d2h) >> e) & 1u) ? probe_us(*c, {{dir, e}}, d, h, n) : 1e30;
+                {
+                    try
+                    {
+                        best[dir][e] = probe_us(*c, {{dir, e}}, d, h, n);
+                    }
+                    catch (const invalid&)
+                    {
+                        best[dir][e] = 1e30;
+                    }
+                }
             double pair_us = 1e30;
             for (int a = 0; a < kProbeEngines; ++a)
                 for (int b = 0; b < kProbeEngines; ++b)
                 {
                     if (a == b || best[0][a] > 1e29 || best[1][b] > 1e29) continue;
                     // (host buffer halves: D2H writes h[0,n), H2D reads h[n,2n) — disjoint)
-                    const double us = probe_us(*c, {{0, a}, {1, b}}, d, h, n);
+                    double us = 1e30;
+                    try
+                    {
+                        us = probe_us(*c, {{0, a}, {1, b}}, d, h, n);
+                    }
+                    catch (const invalid&)
+                    {
+                        continue;
+                    }
                     if (us < pair_us)
                     {
                         pair_us = us;

@@ -96,6 +96,16 @@ class PatternContainer:
     def __call__(self, field):
         return BufferInfo(self, field)
 
+    def filtered(self, ranks, keep: bool) -> "PatternContainer":
+        """The same pattern with only the halos to/from `ranks` (keep=True) or to/from every
+        other rank (keep=False): the reference bulk object's local / remote pattern maps
+        (include/ghex/bulk_communication_object.hpp:330-383)."""
+        rs = [int(r) for r in ranks]
+        h = ctypes.c_void_p()
+        _ghx.call("ghx_pattern_filter", self._h, _ghx.i32_array(rs), len(rs), 1 if keep else 0,
+                  ctypes.byref(h))
+        return type(self)(h.value, self.context, self.domains, self.kind, self.dim)
+
 
 class BufferInfo:
     """buffer_info<pattern, arch, field> (include/ghex/buffer_info.hpp)."""

@@ -259,6 +259,13 @@ int ghx_unstructured_pattern_create(int32_t n_domains, const int32_t* domain_ids
                                     ghx_pattern** out);
 
 int ghx_pattern_destroy(ghx_pattern* p);
+/* A copy of a pattern whose send and receive halo maps keep only the keys whose remote rank is
+ * in `ranks` (keep = 1) or is not (keep = 0); tags and max_tag unchanged. The bulk exchange
+ * splits a pattern this way into its node-local part (puts) and its remote part (a buffered
+ * exchange), as the reference's bulk object splits it into local and remote pattern maps
+ * (include/ghex/bulk_communication_object.hpp:330-383). */
+int ghx_pattern_filter(const ghx_pattern* p, const int32_t* ranks, int32_t n_ranks, int32_t keep,
+                       ghx_pattern** out);
 /* Number of local domains (patterns) of this rank, and the global max tag
  * (pattern_container::max_tag, include/ghex/pattern_container.hpp:78-83). */
 int ghx_pattern_num_domains(const ghx_pattern* p, int32_t* n);

@@ -9,7 +9,7 @@ its send regions straight into the peers' fields through IPC mappings (same GPU 
 GPUs over xGMI on a multi-GPU node). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkrace|bulkgraph|sched|pipe|pipert]"""
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert]"""
 import os
 import sys
 
@@ -50,6 +50,16 @@ def main():
             co.add_field(pc(fd))
             for _ in range(reps):
                 co.exchange().wait()
+        elif mode == "bulkmixed":
+            # two emulated hosts (even / odd ranks): puts between ranks of one host, a host-staged
+            # buffered exchange of the pattern's remote part for the others, one exchange()
+            os.environ["GHX_HOSTNAME"] = f"emulated-host-{rank % 2}"
+            co = ghex_amd.make_bulk_communication_object(ctx, timeout=60,
+                                                         remote_options={"staging": "host"})
+            co.add_field(pc(fd))
+            for _ in range(reps):
+                co.exchange().wait()
+            assert (co._co is not None) == (world > 1)
         elif mode == "bulkrace":
             # device epochs only order the exchanges: per exchange k, on the stream and with no
             # host synchronisation, the field is rewritten (owned cells x f_k, halos -f_k), the

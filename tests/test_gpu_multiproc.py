@@ -52,14 +52,15 @@ def _run(parts, N, Hw, mode):
     assert "bad cells 0" in outs[0]
 
 
-@pytest.mark.parametrize("mode", ["staged", "stagedrt", "bulk", "bulkhost", "bulkrace", "bulkgraph",
-                                  "sched", "pipe", "pipert"])
+@pytest.mark.parametrize("mode", ["staged", "stagedrt", "bulk", "bulkhost", "bulkmixed", "bulkrace",
+                                  "bulkgraph", "sched", "pipe", "pipert"])
 @pytest.mark.parametrize("parts,N,Hw", [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)])
 def test_exchange_multi_process(parts, N, Hw, mode):
     """staged: CommunicationObject(staging="host") over gloo; bulk: zero-copy IPC puts ordered by
     device-side epochs (bulkhost: by host drains + barriers; bulkrace: device epochs as the only
     ordering between rewriting the fields, the exchanges and the halo checks; bulkgraph: the
-    exchange captured into a graph and replayed, one epoch per replay); pipe: the
+    exchange captured into a graph and replayed, one epoch per replay; bulkmixed: two emulated
+    hosts, puts inside a host and a host-staged buffered exchange between them); pipe: the
     pipelined host-staged exchange (per-peer streams, send as each copy lands). Host copies on
     the measured SDMA engines (ghex_amd.staging) by default; stagedrt / pipert: hipMemcpyAsync."""
     _run(parts, N, Hw, mode)

@@ -272,3 +272,22 @@ def test_epochs_flag_block_argument_checks_and_cleanup(ghx):
     assert L.ghx_epochs_unlink(name.encode()) == -1
     assert L.ghx_epochs_peers(None, None, 0, None, 0) == -1
     assert L.ghx_epochs_enqueue(None, 0, None) == -1
+
+
+def test_pattern_filter_splits_local_and_remote_halos():
+    """ghx_pattern_filter (the bulk exchange's local / remote pattern split): keep=True keeps
+    exactly the halos to/from the given ranks, keep=False the others, both in map order, tags
+    and spaces unchanged; the two parts together are the whole pattern."""
+    from tests import helpers as H
+    ranks, gf, gl = H.cube_domains(6, (2, 2, 1))
+    pc = _regular_pattern_abi(ranks, gf, gl, (2,) * 6, (1, 1, 1), 0)
+    for sel in ([1], [1, 2], [0], [3], []):
+        a = pc.filtered(sel, keep=True)
+        b = pc.filtered(sel, keep=False)
+        assert a.max_tag() == b.max_tag() == pc.max_tag()
+        for direction in (0, 1):
+            whole = pc.halos(0, direction)
+            ka, kb = a.halos(0, direction), b.halos(0, direction)
+            assert ka == [h for h in whole if h[1] in sel]
+            assert kb == [h for h in whole if h[1] not in sel]
+            assert sorted(ka + kb) == sorted(whole)
