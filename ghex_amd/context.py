@@ -90,6 +90,9 @@ class Context:
                 _ghx.lib().ghx_rccl_comm_destroy(comm)
 
     def __del__(self):
+        import sys
+        if sys.is_finalizing():
+            return  # process teardown: leave the communicators to it (RCCL's own exit path)
         try:
             self.close()
         except Exception:

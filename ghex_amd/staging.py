@@ -75,6 +75,9 @@ class Copier:
         _ghx.call("ghx_copier_acquire", self.h, stream.cuda_stream)
 
     def __del__(self):
+        import sys
+        if sys.is_finalizing():
+            return  # process teardown releases the engines' signals itself
         try:
             if self.h:
                 _ghx.lib().ghx_copier_destroy(self.h)

@@ -52,9 +52,17 @@ def _run(parts, N, Hw, mode):
     assert "bad cells 0" in outs[0]
 
 
-@pytest.mark.parametrize("mode", ["staged", "stagedrt", "bulk", "bulkhost", "bulkmixed", "bulkrace",
-                                  "bulkgraph", "sched", "pipe", "pipert"])
-@pytest.mark.parametrize("parts,N,Hw", [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)])
+_CASES = [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)]
+
+
+# every mode on the 4-rank case; the main modes on all three (the suite stays a few minutes)
+@pytest.mark.parametrize("parts,N,Hw,mode",
+                         [(c[0], c[1], c[2], m) for c in _CASES
+                          for m in ("staged", "bulk", "sched", "pipe")] +
+                         [(_CASES[1][0], _CASES[1][1], _CASES[1][2], m)
+                          for m in ("stagedrt", "bulkhost", "bulkmixed", "bulkrace", "bulkgraph",
+                                    "pipert")] +
+                         [(_CASES[0][0], _CASES[0][1], _CASES[0][2], "bulkmixed")])
 def test_exchange_multi_process(parts, N, Hw, mode):
     """staged: CommunicationObject(staging="host") over gloo; bulk: zero-copy IPC puts ordered by
     device-side epochs (bulkhost: by host drains + barriers; bulkrace: device epochs as the only
