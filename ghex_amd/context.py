@@ -3,6 +3,7 @@ Python: bindings/python/src/ghex/context.py make_context)."""
 from __future__ import annotations
 
 import ctypes
+import sys
 
 
 class Context:
@@ -90,8 +91,7 @@ class Context:
                 _ghx.lib().ghx_rccl_comm_destroy(comm)
 
     def __del__(self):
-        import sys
-        if sys.is_finalizing():
+        if sys is None or sys.is_finalizing():
             return  # process teardown: leave the communicators to it (RCCL's own exit path)
         try:
             self.close()

@@ -13,6 +13,7 @@ after `acquire(stream)`, which invalidates the L2 caches on that stream first.""
 from __future__ import annotations
 
 import ctypes
+import sys
 import threading
 
 from . import _ghx
@@ -75,8 +76,7 @@ class Copier:
         _ghx.call("ghx_copier_acquire", self.h, stream.cuda_stream)
 
     def __del__(self):
-        import sys
-        if sys.is_finalizing():
+        if sys is None or sys.is_finalizing():
             return  # process teardown releases the engines' signals itself
         try:
             if self.h:
