@@ -116,11 +116,7 @@ struct ghx_copier
     // enqueue one copy; dep: ticket whose completion it waits for on the engine (or ~0)
     uint64_t submit(void* dst, const void* src, size_t n, int dir, uint64_t dep, bool force_engine = true)
     {
-        if (next >= kRing)
-            wait(next - kRing);  // the slot's previous copy must be done before reuse
-        const uint64_t t = next++;
-        hsa_signal_t& s = slot(t);
-        hsa_signal_store_screlease(s, 1);
+        const uint64_t t = next;
         hsa_signal_t d{};
         uint32_t nd = 0;
         if (dep != ~uint64_t(0))
@@ -129,15 +125,23 @@ struct ghx_copier
             d = slot(dep);
             nd = 1;
         }
+        if (t >= kRing) wait(t - kRing);  // the slot's previous copy must be done before reuse
+        hsa_signal_t& s = slot(t);
+        hsa_signal_store_screlease(s, 1);
         const auto eng = hsa_amd_sdma_engine_id_t(1u << engine[dir]);
-        if (dir == 0)
-            hsa_check(hsa_amd_memory_async_copy_on_engine(dst, ag.cpu, src, ag.gpu, n, nd, nd ? &d : nullptr,
-                                                          s, eng, force_engine),
-                      "hsa_amd_memory_async_copy_on_engine(D2H)");
-        else
-            hsa_check(hsa_amd_memory_async_copy_on_engine(dst, ag.gpu, src, ag.cpu, n, nd, nd ? &d : nullptr,
-                                                          s, eng, force_engine),
-                      "hsa_amd_memory_async_copy_on_engine(H2D)");
+        const hsa_status_t st =
+            dir == 0 ? hsa_amd_memory_async_copy_on_engine(dst, ag.cpu, src, ag.gpu, n, nd, nd ? &d : nullptr, s,
+                                                           eng, force_engine)
+                     : hsa_amd_memory_async_copy_on_engine(dst, ag.gpu, src, ag.cpu, n, nd, nd ? &d : nullptr, s,
+                                                           eng, force_engine);
+        if (st != HSA_STATUS_SUCCESS)
+        {
+            // refused: the slot stays free (a signal left at 1 would read as a copy that never ends)
+            hsa_signal_store_screlease(s, 0);
+            hsa_check(st, dir == 0 ? "hsa_amd_memory_async_copy_on_engine(D2H)"
+                                   : "hsa_amd_memory_async_copy_on_engine(H2D)");
+        }
+        next = t + 1;
         return t;
     }
 

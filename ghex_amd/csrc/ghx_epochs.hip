@@ -107,6 +107,23 @@ __global__ __launch_bounds__(64) void k_epoch(epoch_args a, int phase)
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
+// Grid-wide system-scope fences, one wave per workgroup and kFenceGroups workgroups so that
+// every XCD runs some (blocks are dealt round-robin over the 8 XCDs, each with its own L2). The
+// fences in k_epoch run on ONE XCD; a peer's puts land in the target GPU's memory over xGMI, so
+// the source writes back every XCD's L2 before signalling done (k_sys_release) and the target
+// invalidates every XCD's L2 after its wait (k_sys_acquire), before its kernels read the halos.
+constexpr int kFenceGroups = 64;
+
+__global__ __launch_bounds__(64) void k_sys_release()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __builtin_amdgcn_s_waitcnt(0);  // the write-back has completed before the wave ends
+}
+
+__global__ __launch_bounds__(64) void k_sys_acquire()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
 }  // namespace
 }  // namespace ghx
 
@@ -232,14 +249,19 @@ int ghx_epochs_peers(ghx_epochs* ep, const int32_t* sources, int32_t n_sources,
     });
 }
 
-// phase 0: open (before this rank's puts), 1: close (after them)
+// phase 0: open (before this rank's puts), 1: close (after them; bracketed by the grid-wide
+// release / acquire when this rank has targets / sources)
 int ghx_epochs_enqueue(const ghx_epochs* ep, int32_t phase, ghx_stream stream)
 {
     return guarded([&] {
         if (!ep) throw invalid("null epochs");
         if (phase != 0 && phase != 1) throw invalid("phase must be 0 (open) or 1 (close)");
-        hipLaunchKernelGGL(k_epoch, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), ep->args,
-                           int(phase));
+        const auto s = static_cast<hipStream_t>(stream);
+        if (phase == 1 && ep->args.n_tgt > 0)
+            hipLaunchKernelGGL(k_sys_release, dim3(kFenceGroups), dim3(64), 0, s);
+        hipLaunchKernelGGL(k_epoch, dim3(1), dim3(64), 0, s, ep->args, int(phase));
+        if (phase == 1 && ep->args.n_src > 0)
+            hipLaunchKernelGGL(k_sys_acquire, dim3(kFenceGroups), dim3(64), 0, s);
         if (hipGetLastError() != hipSuccess) throw hip_error("k_epoch launch");
         return GHX_OK;
     });
