@@ -268,6 +268,8 @@ struct ghx_put
         if (!ok)
             throw ghx::invalid("source and target iteration spaces do not describe the same "
                                "message bytes (shapes, order, element sizes or row structure differ)");
+        if (from->grouped() || to->grouped())
+            throw ghx::invalid("a put plan takes at most 64 source and 64 target fields (one launch)");
     }
 };
 
@@ -434,7 +436,9 @@ void build_mixed(exchange_plan& ex, int32_t me, const std::vector<ghx_pack_entry
                      [](const ghx_pack_entry& a, const ghx_pack_entry& b) {
                          return a.buffer_slot < b.buffer_slot;
                      });
+    if (ex.spack->grouped()) return;  // more slots than one launch holds: two-launch path
     const splan su(self_e.data(), int(self_e.size()), 1);
+    if (su.grouped()) return;
     std::vector<char> is_self(ex.send.size(), 0);
     for (int i : send_of_recv)
         if (i >= 0) is_self[size_t(i)] = 1;
@@ -602,7 +606,7 @@ int ghx_plan_info(const ghx_plan* plan, uint64_t* bytes, int32_t* n_segments, in
         check_ptr(plan, "plan");
         if (bytes) *bytes = plan->bytes;
         if (n_segments) *n_segments = plan->n_segments;
-        if (n_tiles) *n_tiles = int32_t(plan->n_tiles);
+        if (n_tiles) *n_tiles = int32_t(plan->total_tiles());
         return GHX_OK;
     });
 }
@@ -689,7 +693,7 @@ int ghx_uplan_info(const ghx_uplan* plan, uint64_t* bytes, int32_t* n_segments, 
         check_ptr(plan, "plan");
         if (bytes) *bytes = plan->bytes;
         if (n_segments) *n_segments = plan->n_segments;
-        if (n_tiles) *n_tiles = int32_t(plan->n_tiles);
+        if (n_tiles) *n_tiles = int32_t(plan->total_tiles());
         return GHX_OK;
     });
 }
@@ -971,7 +975,6 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
     return guarded([&] {
         check_ptr(out, "out");
         if (n_items < 1 || !items) throw invalid("need at least one exchange item");
-        if (n_items > GHX_MAX_SLOTS) throw invalid("at most 64 fields per exchange");
         auto ex = std::make_unique<ghx_exchange>();
         ex->n_items = n_items;
         std::vector<ghx_pack_entry> rent;              // receive entries, for build_mixed
@@ -990,7 +993,6 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
             ex->entries[dir] = sent;
             ex->uentries[dir] = uent;
             if (receive) rent = sent;
-            if (bufs.size() > GHX_MAX_SLOTS) throw invalid("more than 64 peer buffers");
             if (!sent.empty())
                 (receive ? ex->sunpack : ex->spack) =
                     std::make_unique<splan>(sent.data(), int(sent.size()), receive ? 1 : 0);

@@ -91,7 +91,8 @@ struct exchange_plan
     bool self_fusable() const
     {
         if (self_ok >= 0) return self_ok == 1;
-        bool ok = !upack && !uunpack && spack && sunpack && send.size() == recv.size();
+        bool ok = !upack && !uunpack && spack && sunpack && send.size() == recv.size() &&
+                  !spack->grouped() && !sunpack->grouped();
         for (size_t i = 0; ok && i < send.size(); ++i)
             ok = send[i].first_id == recv[i].first_id && send[i].second_id == recv[i].second_id &&
                  send[i].size == recv[i].size;

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -160,6 +161,76 @@ void upload(device_tables& dt, const std::vector<Seg>& segs, const std::vector<u
         throw hip_error("hipMemcpy(segments)");
     if (hipMemcpy(dt.tiles, tiles.data(), tb, hipMemcpyHostToDevice) != hipSuccess)
         throw hip_error("hipMemcpy(tiles)");
+}
+// Cut segments (in order) into launch groups of at most GHX_MAX_SLOTS distinct field and buffer
+// slots each; local[k] = segment k's slots inside its group. One group with identity maps
+// (empty) when every caller slot is already below GHX_MAX_SLOTS.
+struct slot_partition
+{
+    std::vector<std::vector<uint32_t>> segs;
+    std::vector<std::vector<int32_t>> fmap, bmap;
+    std::vector<int32_t> lf, lb;
+};
+
+slot_partition partition_slots(const std::vector<int32_t>& gf, const std::vector<int32_t>& gb)
+{
+    slot_partition p;
+    const size_t n = gf.size();
+    p.lf = gf;
+    p.lb = gb;
+    int32_t mf = -1, mb = -1;
+    for (size_t k = 0; k < n; ++k)
+    {
+        mf = std::max(mf, gf[k]);
+        mb = std::max(mb, gb[k]);
+    }
+    if (mf < GHX_MAX_SLOTS && mb < GHX_MAX_SLOTS)
+    {
+        p.segs.emplace_back();
+        for (size_t k = 0; k < n; ++k) p.segs[0].push_back(uint32_t(k));
+        p.fmap.emplace_back();
+        p.bmap.emplace_back();
+        return p;
+    }
+    std::map<int32_t, int32_t> cf, cb;  // current group: caller slot -> local slot
+    for (size_t k = 0; k < n; ++k)
+    {
+        const bool nf = !cf.count(gf[k]), nb = !cb.count(gb[k]);
+        if (p.segs.empty() || cf.size() + nf > size_t(GHX_MAX_SLOTS) ||
+            cb.size() + nb > size_t(GHX_MAX_SLOTS))
+        {
+            p.segs.emplace_back();
+            p.fmap.emplace_back();
+            p.bmap.emplace_back();
+            cf.clear();
+            cb.clear();
+        }
+        auto slot = [](std::map<int32_t, int32_t>& m, std::vector<int32_t>& map, int32_t g) {
+            auto it = m.find(g);
+            if (it != m.end()) return it->second;
+            const int32_t l = int32_t(map.size());
+            m.emplace(g, l);
+            map.push_back(g);
+            return l;
+        };
+        p.lf[k] = slot(cf, p.fmap.back(), gf[k]);
+        p.lb[k] = slot(cb, p.bmap.back(), gb[k]);
+        p.segs.back().push_back(uint32_t(k));
+    }
+    return p;
+}
+
+// Fill a launch's pointer slots from the caller's arrays through a group's maps.
+void fill_slots(uint64_t (&dst)[GHX_MAX_SLOTS], void* const* src, const std::vector<int32_t>& map,
+                int n_identity, const char* what)
+{
+    const int n = map.empty() ? n_identity : int(map.size());
+    for (int i = 0; i < n; ++i)
+    {
+        void* p = src[map.empty() ? i : map[size_t(i)]];
+        if (!p) throw invalid(std::string("null ") + what + " pointer");
+        dst[i] = reinterpret_cast<uint64_t>(p);
+    }
 }
 }  // namespace
 
@@ -332,49 +403,81 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
     tile_bytes = g_tune.tile_bytes;
     if (dir != 0 && dir != 1) throw invalid("direction must be 0 (pack) or 1 (unpack)");
     std::vector<seg_s> segs;
+    std::vector<int32_t> gf, gb;  // caller slots per segment
     for (int e = 0; e < n_entries; ++e)
     {
         const auto& en = entries[e];
         validate_field(en.field);
-        if (en.field_slot < 0 || en.field_slot >= GHX_MAX_SLOTS || en.buffer_slot < 0 ||
-            en.buffer_slot >= GHX_MAX_SLOTS)
-            throw invalid("slot out of range [0, 64)");
+        if (en.field_slot < 0 || en.buffer_slot < 0) throw invalid("negative slot");
         if (en.n_boxes < 0 || (en.n_boxes > 0 && !en.boxes)) throw invalid("bad boxes");
         max_field_slot = std::max(max_field_slot, en.field_slot);
         max_buf_slot = std::max(max_buf_slot, en.buffer_slot);
         uint64_t off = en.buffer_offset;
         for (int b = 0; b < en.n_boxes; ++b)
-            off += add_box_segments(segs, en.field, en.boxes[b], uint16_t(en.field_slot),
-                                    uint16_t(en.buffer_slot), off);
+            off += add_box_segments(segs, en.field, en.boxes[b], 0, 0, off);
+        gf.resize(segs.size(), en.field_slot);
+        gb.resize(segs.size(), en.buffer_slot);
         bytes += off - en.buffer_offset;
     }
-    std::vector<uint32_t> tiles = build_tiles(segs);
     n_segments = int32_t(segs.size());
-    n_tiles = uint32_t(tiles.size() / 2);
-    host_segs = segs;
-    upload(dev, segs, tiles);
+    const slot_partition part = partition_slots(gf, gb);
+    for (size_t g = 0; g < part.segs.size(); ++g)
+    {
+        std::vector<seg_s> gs;
+        for (uint32_t k : part.segs[g])
+        {
+            seg_s x = segs[k];
+            x.field_slot = uint16_t(part.lf[k]);
+            x.buf_slot = uint16_t(part.lb[k]);
+            gs.push_back(x);
+        }
+        std::vector<uint32_t> tiles = build_tiles(gs);
+        if (g == 0)
+        {
+            n_tiles = uint32_t(tiles.size() / 2);
+            host_segs = gs;
+            fmap = part.fmap[0];
+            bmap = part.bmap[0];
+            upload(dev, gs, tiles);
+            continue;
+        }
+        auto grp = std::make_unique<slot_group<seg_s>>();
+        grp->fmap = part.fmap[g];
+        grp->bmap = part.bmap[g];
+        grp->n_tiles = uint32_t(tiles.size() / 2);
+        grp->host_segs = gs;
+        upload(grp->dev, gs, tiles);
+        more.push_back(std::move(grp));
+    }
+}
+
+uint32_t splan::total_tiles() const
+{
+    uint32_t t = n_tiles;
+    for (const auto& g : more) t += g->n_tiles;
+    return t;
 }
 
 int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* stream) const
 {
-    if (n_tiles == 0) return GHX_OK;
+    if (total_tiles() == 0) return GHX_OK;
     if (nf <= max_field_slot || nb <= max_buf_slot) throw invalid("pointer arrays do not cover the plan's slots");
-    if (!dev.segs) throw hip_error("plan has no device tables (no HIP device at creation)");
-    kargs a{};
-    a.segs = dev.segs;
-    a.tile_seg = dev.tiles;
-    a.n_tiles = n_tiles;
-    for (int i = 0; i <= max_field_slot; ++i)
-    {
-        if (!fptr[i]) throw invalid("null field pointer");
-        a.field_ptr[i] = reinterpret_cast<uint64_t>(fptr[i]);
-    }
-    for (int i = 0; i <= max_buf_slot; ++i)
-    {
-        if (!bptr[i]) throw invalid("null buffer pointer");
-        a.buf_ptr[i] = reinterpret_cast<uint64_t>(bptr[i]);
-    }
-    return launch_structured(a, direction, stream, grid_for_tiles(n_tiles));
+    auto run = [&](const device_tables& dt, uint32_t nt, const std::vector<int32_t>& fm,
+                   const std::vector<int32_t>& bm) {
+        if (nt == 0) return int(GHX_OK);
+        if (!dt.segs) throw hip_error("plan has no device tables (no HIP device at creation)");
+        kargs a{};
+        a.segs = dt.segs;
+        a.tile_seg = dt.tiles;
+        a.n_tiles = nt;
+        fill_slots(a.field_ptr, fptr, fm, max_field_slot + 1, "field");
+        fill_slots(a.buf_ptr, bptr, bm, max_buf_slot + 1, "buffer");
+        return launch_structured(a, direction, stream, grid_for_tiles(nt));
+    };
+    int rc = run(dev, n_tiles, fmap, bmap);
+    for (size_t g = 0; rc == GHX_OK && g < more.size(); ++g)
+        rc = run(more[g]->dev, more[g]->n_tiles, more[g]->fmap, more[g]->bmap);
+    return rc;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -395,15 +498,14 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         size_t off;
     };
     std::vector<pending> pend;
+    std::vector<int32_t> gf, gb;  // caller slots per segment
     size_t lid_bytes = 0;
     for (int e = 0; e < n_entries; ++e)
     {
         const auto& en = entries[e];
         const auto& d = en.data;
         if (d.elem_size < 1 || d.levels < 1) throw invalid("bad unstructured data descriptor");
-        if (en.field_slot < 0 || en.field_slot >= GHX_MAX_SLOTS || en.buffer_slot < 0 ||
-            en.buffer_slot >= GHX_MAX_SLOTS)
-            throw invalid("slot out of range [0, 64)");
+        if (en.field_slot < 0 || en.buffer_slot < 0) throw invalid("negative slot");
         if (en.n_lids < 0 || (en.n_lids > 0 && !en.lids)) throw invalid("bad index list");
         max_field_slot = std::max(max_field_slot, en.field_slot);
         max_buf_slot = std::max(max_buf_slot, en.buffer_slot);
@@ -418,9 +520,7 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
             if (en.lids[i] < 0) throw invalid("negative local index");
             if (en.lids[i] >= (int64_t(1) << 31)) wide = true;
         }
-        seg_u s{};
-        s.field_slot = uint16_t(en.field_slot);
-        s.buf_slot = uint16_t(en.buffer_slot);
+        seg_u s{};  // slots: set per launch group below
         s.buf_off = en.buffer_offset;
         s.n = uint32_t(en.n_lids);
         s.index_stride_b = d.index_stride * elem;
@@ -475,12 +575,11 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         lid_bytes += size_t(en.n_lids) * (wide ? 8 : 4);
         pend.push_back(pe);
         segs.push_back(s);
+        gf.push_back(en.field_slot);
+        gb.push_back(en.buffer_slot);
         bytes += uint64_t(total);
     }
-    std::vector<uint32_t> tiles = build_tiles(segs);
     n_segments = int32_t(segs.size());
-    n_tiles = uint32_t(tiles.size() / 2);
-    host_segs = segs;
     if (!segs.empty() && have_device())
     {
         std::vector<unsigned char> host(lid_bytes);
@@ -501,40 +600,75 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         if (hipMemcpy(dev.lids, host.data(), lid_bytes, hipMemcpyHostToDevice) != hipSuccess)
             throw hip_error("hipMemcpy(lids)");
         for (auto& p : pend) segs[p.seg].lids = static_cast<char*>(dev.lids) + p.off;
-        void* keep = dev.lids;
-        dev.lids = nullptr;  // upload() releases; re-attach after
-        upload(dev, segs, tiles);
-        dev.lids = keep;
     }
+    const slot_partition part = partition_slots(gf, gb);
+    for (size_t g = 0; g < part.segs.size(); ++g)
+    {
+        std::vector<seg_u> gs;
+        for (uint32_t k : part.segs[g])
+        {
+            seg_u x = segs[k];
+            x.field_slot = uint16_t(part.lf[k]);
+            x.buf_slot = uint16_t(part.lb[k]);
+            gs.push_back(x);
+        }
+        std::vector<uint32_t> tiles = build_tiles(gs);
+        if (g == 0)
+        {
+            n_tiles = uint32_t(tiles.size() / 2);
+            host_segs = gs;
+            fmap = part.fmap[0];
+            bmap = part.bmap[0];
+            void* keep = dev.lids;
+            dev.lids = nullptr;  // upload() releases; re-attach after (the groups share it)
+            upload(dev, gs, tiles);
+            dev.lids = keep;
+            continue;
+        }
+        auto grp = std::make_unique<slot_group<seg_u>>();
+        grp->fmap = part.fmap[g];
+        grp->bmap = part.bmap[g];
+        grp->n_tiles = uint32_t(tiles.size() / 2);
+        grp->host_segs = gs;
+        upload(grp->dev, gs, tiles);
+        more.push_back(std::move(grp));
+    }
+}
+
+uint32_t uplan::total_tiles() const
+{
+    uint32_t t = n_tiles;
+    for (const auto& g : more) t += g->n_tiles;
+    return t;
 }
 
 int uplan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* stream) const
 {
-    if (n_tiles == 0) return GHX_OK;
+    if (total_tiles() == 0) return GHX_OK;
     if (nf <= max_field_slot || nb <= max_buf_slot) throw invalid("pointer arrays do not cover the plan's slots");
-    if (!dev.segs) throw hip_error("plan has no device tables (no HIP device at creation)");
-    kargs a{};
-    a.segs = dev.segs;
-    a.tile_seg = dev.tiles;
-    a.n_tiles = n_tiles;
-    for (int i = 0; i <= max_field_slot; ++i)
-    {
-        if (!fptr[i]) throw invalid("null field pointer");
-        a.field_ptr[i] = reinterpret_cast<uint64_t>(fptr[i]);
-    }
-    for (int i = 0; i <= max_buf_slot; ++i)
-    {
-        if (!bptr[i]) throw invalid("null buffer pointer");
-        a.buf_ptr[i] = reinterpret_cast<uint64_t>(bptr[i]);
-    }
-    // the run-path kernel when every segment qualifies with these pointers: flagged by the
-    // planner, whole 16-B chunks per tile, 16-B aligned buffer ranges, field base aligned to L
-    bool runs = !host_segs.empty();
-    for (const seg_u& s : host_segs)
-        runs = runs && s.runs && s.tile_bytes % 16 == 0 &&
-               (a.buf_ptr[s.buf_slot] + s.buf_off) % 16 == 0 &&
-               a.field_ptr[s.field_slot] % s.row_bytes == 0;
-    return launch_unstructured(a, direction, stream, grid_for_tiles(n_tiles), runs);
+    auto run = [&](const device_tables& dt, uint32_t nt, const std::vector<int32_t>& fm,
+                   const std::vector<int32_t>& bm, const std::vector<seg_u>& hs) {
+        if (nt == 0) return int(GHX_OK);
+        if (!dt.segs) throw hip_error("plan has no device tables (no HIP device at creation)");
+        kargs a{};
+        a.segs = dt.segs;
+        a.tile_seg = dt.tiles;
+        a.n_tiles = nt;
+        fill_slots(a.field_ptr, fptr, fm, max_field_slot + 1, "field");
+        fill_slots(a.buf_ptr, bptr, bm, max_buf_slot + 1, "buffer");
+        // the run-path kernel when every segment qualifies with these pointers: flagged by the
+        // planner, whole 16-B chunks per tile, 16-B aligned buffer ranges, field base aligned to L
+        bool runs = !hs.empty();
+        for (const seg_u& s : hs)
+            runs = runs && s.runs && s.tile_bytes % 16 == 0 &&
+                   (a.buf_ptr[s.buf_slot] + s.buf_off) % 16 == 0 &&
+                   a.field_ptr[s.field_slot] % s.row_bytes == 0;
+        return launch_unstructured(a, direction, stream, grid_for_tiles(nt), runs);
+    };
+    int rc = run(dev, n_tiles, fmap, bmap, host_segs);
+    for (size_t g = 0; rc == GHX_OK && g < more.size(); ++g)
+        rc = run(more[g]->dev, more[g]->n_tiles, more[g]->fmap, more[g]->bmap, more[g]->host_segs);
+    return rc;
 }
 
 }  // namespace ghx

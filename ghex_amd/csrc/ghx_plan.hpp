@@ -1,6 +1,7 @@
 // ghx_plan.hpp — host planner objects behind the opaque C handles.
 #pragma once
 
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -36,17 +37,36 @@ void upload_segments(device_tables& dt, const std::vector<seg_s>& segs);
 uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, const ghx_box& box,
                           uint16_t field_slot, uint16_t buf_slot, uint64_t buf_off);
 
+// Launch groups. A launch carries at most GHX_MAX_SLOTS field and buffer pointers (kargs is
+// passed by value); a plan whose entries use more slots than that (many fields in one exchange,
+// or many domain-pair buffers: a rank holding many domains) is cut into groups of segments in
+// entry order, each with its own slot maps (local slot -> the caller's slot) and tables, and
+// executes as one launch per group on the same stream. The reference has no such limit
+// (include/ghex/communication_object.hpp:1003-1067 allocates any number of buffers).
+template<typename Seg>
+struct slot_group
+{
+    std::vector<int32_t> fmap, bmap;  // local slot -> caller slot; empty: identity
+    uint32_t n_tiles = 0;
+    std::vector<Seg> host_segs;
+    device_tables dev;
+};
+
 // structured fused plan
 struct splan
 {
     int direction = 0;
     uint64_t bytes = 0;
     int32_t n_segments = 0;
-    uint32_t n_tiles = 0;
+    uint32_t n_tiles = 0;      // the first launch group's (the whole plan's when not grouped)
     uint32_t tile_bytes = kTileBytes;
-    int max_field_slot = -1, max_buf_slot = -1;
-    std::vector<seg_s> host_segs;
+    int max_field_slot = -1, max_buf_slot = -1;  // caller slots
+    std::vector<seg_s> host_segs;                // the first group's, local slots
     device_tables dev;
+    std::vector<int32_t> fmap, bmap;             // the first group's slot maps (empty: identity)
+    std::vector<std::unique_ptr<slot_group<seg_s>>> more;  // further launch groups
+    bool grouped() const { return !fmap.empty() || !bmap.empty() || !more.empty(); }
+    uint32_t total_tiles() const;
     splan(const ghx_pack_entry* entries, int n_entries, int direction);
     int execute(void* const* fptr, int nf, void* const* bptr, int nb, void* stream) const;
 };
@@ -62,6 +82,10 @@ struct uplan
     int max_field_slot = -1, max_buf_slot = -1;
     device_tables dev;
     std::vector<seg_u> host_segs;  // for the launch-time choice of the run-path kernel
+    std::vector<int32_t> fmap, bmap;
+    std::vector<std::unique_ptr<slot_group<seg_u>>> more;
+    bool grouped() const { return !fmap.empty() || !bmap.empty() || !more.empty(); }
+    uint32_t total_tiles() const;
     uplan(const ghx_upack_entry* entries, int n_entries, int direction);
     int execute(void* const* fptr, int nf, void* const* bptr, int nb, void* stream) const;
 };

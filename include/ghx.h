@@ -41,7 +41,8 @@ typedef enum ghx_status
 typedef void* ghx_stream;
 
 #define GHX_MAX_DIM 4     /* 3 spatial dims + 1 component axis (bindings/python/src/_pyghex/structured/types.hpp:31-63) */
-#define GHX_MAX_SLOTS 64  /* field / buffer pointer slots per plan execution */
+#define GHX_MAX_SLOTS 64  /* field / buffer pointer slots per kernel launch; a plan whose entries
+                             use more is executed as one launch per group of <= 64 (any slot >= 0) */
 
 /* Process-wide tuning knobs (development / benchmarking; defaults are the measured best):
  * "grid_cap" (max workgroups, 0 = one per tile), "tile_bytes" (buffer bytes per workgroup tile),

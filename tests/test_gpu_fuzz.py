@@ -1,0 +1,154 @@
+"""Seeded random structured exchanges, device path against the oracle.
+
+Each case draws a non-cubic periodic-or-not global grid, an uneven decomposition into boxes, 1-3
+domains per rank (ranks emulated in one process), two pattern containers with independent
+asymmetric halos (0-3 cells per side, wider than a domain at times), and 1-3 fields of mixed
+element types (1, 2, 4 and 8 bytes) with random layout maps and extra allocation padding
+(offsets larger than the halo, extents larger than domain + halos). Every cell of every field
+after the exchange — halos, interior and padding — equals the oracle's exchange, and every
+packed send buffer equals the oracle's bytes (alignment pads masked: the reference never writes
+them either, communication_object.hpp:1059-1065). The oracle follows
+include/ghex/structured/pattern.hpp:214-571 (patterns) and pack_kernels.hpp:62-158 (bytes)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = [np.uint8, np.int16, np.float32, np.int32, np.float64, np.int64]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ghex_amd
+    ghex_amd.native_library()
+
+
+def _split(n, parts, rng):
+    """n cells into `parts` non-empty intervals of random sizes: [(first, last)]."""
+    cuts = sorted(rng.choice(np.arange(1, n), size=parts - 1, replace=False)) if parts > 1 else []
+    b = [0] + [int(c) for c in cuts] + [n]
+    return [(b[i], b[i + 1] - 1) for i in range(parts)]
+
+
+def draw_case(seed):
+    rng = np.random.default_rng(seed)
+    G = [int(rng.integers(3, 15)) for _ in range(3)]
+    parts = [int(rng.integers(1, min(3, G[d]) + 1)) for d in range(3)]
+    ivals = [_split(G[d], parts[d], rng) for d in range(3)]
+    boxes = [((ivals[0][i][0], ivals[1][j][0], ivals[2][k][0]),
+              (ivals[0][i][1], ivals[1][j][1], ivals[2][k][1]))
+             for k in range(parts[2]) for j in range(parts[1]) for i in range(parts[0])]
+    nd = len(boxes)
+    nr = int(rng.integers(1, min(4, nd) + 1))
+    owner = [r for r in range(nr)] + [int(rng.integers(0, nr)) for _ in range(nd - nr)]
+    owner = [owner[i] for i in rng.permutation(nd)]
+    ids = [int(x) for x in rng.permutation(nd) + 10]
+    ranks = [[] for _ in range(nr)]
+    for b, (f, l) in enumerate(boxes):
+        ranks[owner[b]].append(orc.RegularDomain(ids[b], f, l))
+    halos = {pc: tuple(int(h) for h in rng.integers(0, 4, size=6)) for pc in (1, 2)}
+    periodic = tuple(int(p) for p in rng.integers(0, 2, size=3))
+    nf = int(rng.integers(1, 4))
+    fields = []
+    for _ in range(nf):
+        fields.append({"dtype": DTYPES[int(rng.integers(0, len(DTYPES)))],
+                       "layout": tuple(int(x) for x in rng.permutation(3)),
+                       "pc": int(rng.integers(1, 3)),
+                       "pad": [(int(rng.integers(0, 3)), int(rng.integers(0, 3))) for _ in range(3)]})
+    return {"G": G, "ranks": ranks, "halos": halos, "periodic": periodic, "fields": fields,
+            "mixed": bool(rng.integers(0, 2)), "seed": seed}
+
+
+def _alloc(dom, f, halos_max, rng):
+    """Random-valued field storage for `dom` (memory order by the layout map) + its FieldSpec."""
+    dt = np.dtype(f["dtype"])
+    offs, exts = [], []
+    for d in range(3):
+        n = dom.last[d] - dom.first[d] + 1
+        lo, hi = halos_max[2 * d] + f["pad"][d][0], halos_max[2 * d + 1] + f["pad"][d][1]
+        offs.append(lo)
+        exts.append(max(2, lo + n + hi))  # extent 1 would tie two strides (layout ambiguity)
+    order = sorted(range(3), key=lambda d: f["layout"][d])  # slowest ... fastest
+    shape = tuple(exts[d] for d in order)
+    raw = rng.integers(0, 256, size=int(np.prod(shape)) * dt.itemsize, dtype=np.uint8)
+    a = raw.view(dt).reshape(shape).copy()
+    return a, orc.FieldSpec(a, dt.itemsize, f["layout"], tuple(offs), tuple(exts))
+
+
+def run_case(case):
+    from ghex_amd import _ghx
+    from ghex_amd.structured import regular as R
+    from tests.gpu_util import FakeContext, device_field, emulated_exchange
+    ranks, nr = case["ranks"], len(case["ranks"])
+    gf, gl = (0, 0, 0), tuple(g - 1 for g in case["G"])
+    per = case["periodic"]
+    hmax = tuple(max(case["halos"][1][i], case["halos"][2][i]) for i in range(6))
+    pat_o = {pc: orc.regular_make_pattern(ranks, gf, gl, case["halos"][pc], per) for pc in (1, 2)}
+    table = {r: [(d.id, d.first, d.last) for d in ranks[r]] for r in range(nr)}
+    rng = np.random.default_rng(case["seed"] + 1000)
+    cos, bis_all, pairs, ranks_fields = [], [], [], []
+    for r in range(nr):
+        ctx = FakeContext(r, nr, table)
+        dds = [R.DomainDescriptor(d.id, d.first, d.last) for d in ranks[r]]
+        pcs = {pc: R.make_pattern(ctx, R.HaloGenerator(gf, gl, case["halos"][pc], per), dds)
+               for pc in (1, 2)}
+        bis, rf = [], []
+        for f in case["fields"]:  # exchange() argument order: field-major, then domains
+            for li, dom in enumerate(ranks[r]):
+                a, spec = _alloc(dom, f, hmax, rng)
+                base, logical = device_field(a.copy(), f["layout"])
+                fd = R.make_field_descriptor(dds[li], logical, spec.offsets, spec.extents)
+                assert fd.layout == f["layout"]
+                bis.append(pcs[f["pc"]](fd))
+                pairs.append((base, a))
+                rf.append((spec, dom.id, li, f["pc"]))
+        cos.append(R.make_communication_object(ctx))
+        bis_all.append(bis)
+        ranks_fields.append(rf)
+    obufs = orc.regular_exchange(ranks_fields, pat_o, nr)
+    _ghx.call("ghx_tune", b"mixed_always", 1 if case["mixed"] else 0)
+    try:
+        plans, bufs = emulated_exchange(cos, bis_all, mixed=case["mixed"])
+    finally:
+        _ghx.call("ghx_tune", b"reset", 0)
+    for base, a in pairs:
+        np.testing.assert_array_equal(base.cpu().numpy(), a)
+    for r in range(nr):
+        items = [(k, f[1], pat_o[f[3]][r][f[2]], f[0].elem, f[0].data.dtype.alignment, 1, 0)
+                 for k, f in enumerate(ranks_fields[r])]
+        pb = orc.plan_buffers(items, receive=False)
+        for i, x in enumerate(plans[r].send):
+            ob = obufs[(r, x["pair"])]
+            assert ob.size == x["size"]
+            b = pb[x["pair"]]
+            m = np.zeros(b.size, dtype=bool)
+            for pf in b.fields:
+                elem = ranks_fields[r][pf.field_index][0].elem
+                n = sum(isp.size() for isp in pf.boxes) * elem
+                m[pf.offset:pf.offset + n] = True
+            np.testing.assert_array_equal(bufs[r][0][i][:x["size"]].cpu().numpy()[m], ob[m])
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_structured_exchange(seed):
+    run_case(draw_case(seed))
+
+
+def test_more_slots_than_one_launch_holds():
+    """One rank with 8 domains of a periodic 6^3 grid and 70 fields: 560 exchange items (field
+    slots) over 56 domain-pair buffers, far beyond the 64 field pointers one launch carries —
+    the plans run as launch groups (ghx_plan.cpp partition_slots), bit-exact as ever. (Random
+    seed 7 above has 178 buffers: the buffer side of the same limit.)"""
+    rng = np.random.default_rng(64)
+    doms = [orc.RegularDomain(100 + i, (3 * (i % 2), 3 * (i // 2 % 2), 3 * (i // 4)),
+                              (3 * (i % 2) + 2, 3 * (i // 2 % 2) + 2, 3 * (i // 4) + 2))
+            for i in range(8)]
+    fields = [{"dtype": DTYPES[k % len(DTYPES)], "layout": tuple(int(x) for x in rng.permutation(3)),
+               "pc": 1 + k % 2, "pad": [(k % 2, k % 3), (0, 1), (1, 0)]} for k in range(70)]
+    run_case({"G": [6, 6, 6], "ranks": [doms], "halos": {1: (1,) * 6, 2: (2, 1, 0, 2, 1, 1)},
+              "periodic": (1, 1, 1), "fields": fields, "mixed": False, "seed": 64})

@@ -246,6 +246,37 @@ def test_put_plan_pairs_matching_sides_and_refuses_mismatch():
     assert b"same message bytes" in L.ghx_last_error()
 
 
+def test_plans_beyond_64_slots_are_cut_into_launch_groups():
+    """A launch carries at most 64 field and 64 buffer pointers; a plan whose entries use more
+    slots (many fields in one exchange, many domain-pair buffers) is planned in launch groups of
+    <= 64 slots each: every slot accepted, every tile kept (the sum over entries planned alone).
+    Host-side planning only here; tests/test_gpu_fuzz.py runs such exchanges on the device."""
+    import ctypes
+    from ghex_amd import _ghx
+    L = _ghx.lib()
+    ents = _put_entries([(3 + k % 5, 1 + k % 3, k % 2) for k in range(150)])
+    singles = 0
+    for k, (e, _) in enumerate(ents):
+        e.field_slot, e.buffer_slot = k, 149 - k  # 150 distinct slots on both sides
+        h = ctypes.c_void_p()
+        assert L.ghx_plan_create(ctypes.byref(e), 1, 0, ctypes.byref(h)) == 0
+        nt = ctypes.c_int32()
+        assert L.ghx_plan_info(h, None, None, ctypes.byref(nt)) == 0
+        singles += nt.value
+        assert L.ghx_plan_destroy(h) == 0
+    arr = (_ghx.PackEntry * len(ents))(*[e for e, _ in ents])
+    h = ctypes.c_void_p()
+    assert L.ghx_plan_create(arr, len(ents), 0, ctypes.byref(h)) == 0, L.ghx_last_error()
+    nb, ns, nt = ctypes.c_uint64(), ctypes.c_int32(), ctypes.c_int32()
+    assert L.ghx_plan_info(h, ctypes.byref(nb), ctypes.byref(ns), ctypes.byref(nt)) == 0
+    assert nt.value == singles and ns.value >= 150
+    assert L.ghx_plan_destroy(h) == 0
+    e, _ = ents[0]
+    e.field_slot = -1
+    assert L.ghx_plan_create(ctypes.byref(e), 1, 0, ctypes.byref(h)) == -1
+    assert b"negative slot" in L.ghx_last_error()
+
+
 def test_epochs_flag_block_argument_checks_and_cleanup(ghx):
     """ghx_epochs_* (device-side access epochs of the bulk exchange) without a GPU: bad names,
     world/rank and timeouts are refused; a creating rank that cannot register the block (no
