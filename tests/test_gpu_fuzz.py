@@ -152,3 +152,131 @@ def test_more_slots_than_one_launch_holds():
                "pc": 1 + k % 2, "pad": [(k % 2, k % 3), (0, 1), (1, 0)]} for k in range(70)]
     run_case({"G": [6, 6, 6], "ranks": [doms], "halos": {1: (1,) * 6, 2: (2, 1, 0, 2, 1, 1)},
               "periodic": (1, 1, 1), "fields": fields, "mixed": False, "seed": 64})
+
+
+# ---------------------------------------------------------------------------------------------
+# unstructured: random meshes, the reference tests' halo property
+# ---------------------------------------------------------------------------------------------
+UDTYPES = [np.float64, np.float32, np.int32, np.int64, np.int16]
+
+
+def draw_unstructured(seed):
+    """Ranks (1-4) holding 1-2 domains each; every domain owns 5-60 cells with globally unique
+    gids and holds a halo of gids owned by other domains (repeats allowed: a gid may be the halo
+    of one domain twice, unstructured/user_concepts.hpp:88-113), all in a random storage order."""
+    rng = np.random.default_rng(seed)
+    nr = int(rng.integers(1, 5))
+    doms = []  # (rank, id, inner gids)
+    next_gid, did = 1000, 0
+    for r in range(nr):
+        for _ in range(int(rng.integers(1, 3))):
+            n = int(rng.integers(5, 61))
+            doms.append([r, did, list(range(next_gid, next_gid + n))])
+            next_gid += n + int(rng.integers(0, 50))
+            did += 1
+    out = []
+    for k, (r, i, inner) in enumerate(doms):
+        others = [g for kk, d in enumerate(doms) if kk != k for g in d[2]]
+        nh = int(rng.integers(0, min(len(others), 30) + 1)) if others else 0
+        halo = [int(g) for g in rng.choice(others, size=nh, replace=False)] if nh else []
+        if halo and rng.random() < 0.3:
+            halo.append(halo[0])  # a repeated halo gid: two outer cells of one gid
+        gids = inner + halo
+        perm = rng.permutation(len(gids))
+        gids = [gids[p] for p in perm]
+        outer = sorted(int(np.where(perm == len(inner) + h)[0][0]) for h in range(len(halo)))
+        out.append({"rank": r, "id": i, "gids": gids, "outer": outer})
+    fields = []
+    for _ in range(int(rng.integers(1, 3))):
+        fields.append({"dtype": UDTYPES[int(rng.integers(0, len(UDTYPES)))],
+                       "levels": int(rng.integers(1, 5)), "first": bool(rng.integers(0, 2)),
+                       "pad": int(rng.integers(0, 3))})
+    return {"nr": nr, "doms": out, "fields": fields, "seed": seed}
+
+
+def _ufield(torch, n, f, rng):
+    """Device tensor (n, levels) in the field's layout: levels_first rows padded by `pad`
+    values (outer stride levels + pad), or levels_last (level-major, stride n); random bytes."""
+    dt, L = np.dtype(f["dtype"]), f["levels"]
+    if f["first"]:
+        shape, cols = (n, L + f["pad"]), slice(0, L)
+    else:
+        shape = (L, n)
+    raw = rng.integers(0, 256, size=int(np.prod(shape)) * dt.itemsize, dtype=np.uint8)
+    a = raw.view(dt).reshape(shape).copy()
+    t = torch.from_numpy(a).cuda()
+    view = t[:, cols] if f["first"] else t.t()
+    if L == 1 and f["first"] and f["pad"] == 0:
+        view = t[:, 0]  # the 1-D form
+    return t, view, a
+
+
+def run_unstructured(case):
+    import torch
+    from ghex_amd import unstructured as U
+    from tests.gpu_util import FakeContext, emulated_exchange
+    nr = case["nr"]
+    table = {r: [(d["id"], d["gids"], d["outer"], None) for d in case["doms"] if d["rank"] == r]
+             for r in range(nr)}
+    rng = np.random.default_rng(case["seed"] + 7)
+    cos, bis_all, recs = [], [], []
+    for r in range(nr):
+        ctx = FakeContext(r, nr, table)
+        mine = [d for d in case["doms"] if d["rank"] == r]
+        dds = [U.DomainDescriptor(d["id"], d["gids"], d["outer"]) for d in mine]
+        pc = U.make_pattern(ctx, U.HaloGenerator(), dds)
+        bis = []
+        for f in case["fields"]:
+            for dd, d in zip(dds, mine):
+                t, view, a = _ufield(torch, len(d["gids"]), f, rng)
+                bis.append(pc(U.make_field_descriptor(dd, view)))
+                recs.append((f, d, t, a))
+        cos.append(U.make_communication_object(ctx))
+        bis_all.append(bis)
+    emulated_exchange(cos, bis_all)
+    # expected: every outer cell holds, on every level, the value of the cell that owns its gid
+    for fi, f in enumerate(case["fields"]):
+        owner = {}
+        for (ff, d, t, a) in recs:
+            if ff is not f:
+                continue
+            outer = set(d["outer"])
+            for lid, g in enumerate(d["gids"]):
+                if lid not in outer:
+                    owner[g] = a[lid, :f["levels"]] if f["first"] else a[:, lid]
+        for (ff, d, t, a) in recs:
+            if ff is not f:
+                continue
+            got = t.cpu().numpy()
+            exp = a.copy()
+            for lid in d["outer"]:
+                v = owner[d["gids"][lid]]
+                if f["first"]:
+                    exp[lid, :f["levels"]] = v
+                else:
+                    exp[:, lid] = v
+            np.testing.assert_array_equal(got.view(np.uint8), exp.view(np.uint8))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_unstructured_exchange(seed):
+    run_unstructured(draw_unstructured(seed))
+
+
+def test_unstructured_more_buffers_than_one_launch_holds():
+    """2 ranks x 40 domains, each domain's halo drawn from 12 other domains: ~960 domain-pair
+    buffers and 80 field slots per rank, unpacked through launch groups of <= 64 slots."""
+    rng = np.random.default_rng(99)
+    doms, gid = [], 5000
+    for k in range(80):
+        doms.append({"rank": k // 40, "id": k, "inner": list(range(gid, gid + 6))})
+        gid += 6
+    out = []
+    for k, d in enumerate(doms):
+        src = [int(x) for x in rng.choice([j for j in range(80) if j != k], size=12, replace=False)]
+        halo = [doms[j]["inner"][int(rng.integers(0, 6))] for j in src]
+        gids = d["inner"] + halo
+        out.append({"rank": d["rank"], "id": d["id"], "gids": gids,
+                    "outer": list(range(6, 6 + len(halo)))})
+    run_unstructured({"nr": 2, "doms": out, "seed": 99,
+                      "fields": [{"dtype": np.float64, "levels": 2, "first": True, "pad": 1}]})
