@@ -213,28 +213,33 @@ class BulkCommunicationObject:
             _ghx.call("ghx_ipc_import", h, f["offset"], ctypes.byref(base), ctypes.byref(ptr))
             self._imports.append(base.value)
             ptr_of[(tr, ti)] = ptr.value
-        # group messages into put plans of <= 64 messages and <= 64 target fields
-        chunk, dsts = [], []
+        # group messages into put plans (one launch each) of <= 64 messages, <= 64 source and
+        # <= 64 target fields
+        chunk, srcs, dsts = [], [], []
         for m in msgs + [None]:
-            if m is None or len(chunk) == MAX_SLOTS or (m[2] not in dsts and len(dsts) == MAX_SLOTS):
+            if (m is None or len(chunk) == MAX_SLOTS or
+                    (m[0] not in srcs and len(srcs) == MAX_SLOTS) or
+                    (m[2] not in dsts and len(dsts) == MAX_SLOTS)):
                 if chunk:
-                    self._make_put(chunk, dsts, allr, ptr_of)
-                chunk, dsts = [], []
+                    self._make_put(chunk, srcs, dsts, allr, ptr_of)
+                chunk, srcs, dsts = [], [], []
                 if m is None:
                     break
+            if m[0] not in srcs:
+                srcs.append(m[0])
             if m[2] not in dsts:
                 dsts.append(m[2])
             chunk.append(m)
         self._initialized = True
 
-    def _make_put(self, chunk, dsts, allr, ptr_of):
+    def _make_put(self, chunk, srcs, dsts, allr, ptr_of):
         n = len(chunk)
         src = (_ghx.PackEntry * n)()
         dst = (_ghx.PackEntry * n)()
         keep = [src, dst]
         for b, (k, sps, tgt, tsps) in enumerate(chunk):
             tdesc = _ghx.FieldDesc.from_buffer_copy(allr[tgt[0]]["fields"][tgt[1]]["desc"])
-            for e, desc, slot, spaces in ((src[b], self._bis[k].field.desc, k, sps),
+            for e, desc, slot, spaces in ((src[b], self._bis[k].field.desc, srcs.index(k), sps),
                                           (dst[b], tdesc, dsts.index(tgt), tsps)):
                 arr = (_ghx.Box * max(1, len(spaces)))()
                 for i, (lf, ll) in enumerate(spaces):
@@ -249,10 +254,10 @@ class BulkCommunicationObject:
                 e.n_boxes = len(spaces)
         h = ctypes.c_void_p()
         _ghx.call("ghx_put_create", src, n, dst, n, ctypes.byref(h))
-        sp = _ghx.ptr_array([bi.field.data_ptr() for bi in self._bis])
+        sp = _ghx.ptr_array([self._bis[k].field.data_ptr() for k in srcs])
         dp = _ghx.ptr_array([ptr_of[t] for t in dsts])
         self._keep.append(keep)
-        self._puts.append((h, sp, len(self._bis), dp, len(dsts)))
+        self._puts.append((h, sp, len(srcs), dp, len(dsts)))
 
     def _epochs_attach(self, name, create, world, rank):
         h = ctypes.c_void_p()

@@ -117,13 +117,12 @@ class bulk_communication_object
     struct put
     {
         ghx_put* h = nullptr;
-        std::vector<void*> dst;
+        std::vector<void*> src, dst;  // the plan's source / target field slots
     };
 
     context* m_ctx;
     hipStream_t m_stream = nullptr;
     std::vector<local_field> m_fields;
-    std::vector<void*> m_src;
     std::vector<put> m_puts;
     std::vector<void*> m_imports;
     bool m_init = false;
@@ -243,8 +242,9 @@ class bulk_communication_object
         const std::vector<ghx_box>* tboxes;
     };
 
-    void make_put(const std::vector<msg>& chunk, const std::vector<std::pair<int, int>>& dsts,
-                  const std::vector<remote_rank>& all, const std::map<std::pair<int, int>, void*>& ptr_of)
+    void make_put(const std::vector<msg>& chunk, const std::vector<int>& srcs,
+                  const std::vector<std::pair<int, int>>& dsts, const std::vector<remote_rank>& all,
+                  const std::map<std::pair<int, int>, void*>& ptr_of)
     {
         const auto n = chunk.size();
         std::vector<ghx_pack_entry> src(n), dst(n);
@@ -254,7 +254,7 @@ class bulk_communication_object
             std::memset(&src[b], 0, sizeof(ghx_pack_entry));
             std::memset(&dst[b], 0, sizeof(ghx_pack_entry));
             src[b].field = m_fields[std::size_t(m.src)].desc;
-            src[b].field_slot = m.src;
+            src[b].field_slot = std::int32_t(std::find(srcs.begin(), srcs.end(), m.src) - srcs.begin());
             src[b].buffer_slot = std::int32_t(b);
             src[b].boxes = m.sboxes.data();
             src[b].n_boxes = std::int32_t(m.sboxes.size());
@@ -267,6 +267,7 @@ class bulk_communication_object
         }
         put p;
         check_ghx(ghx_put_create(src.data(), std::int32_t(n), dst.data(), std::int32_t(n), &p.h), "ghx_put_create");
+        for (int k : srcs) p.src.push_back(m_fields[std::size_t(k)].data);
         for (const auto& t : dsts) p.dst.push_back(ptr_of.at(t));
         m_puts.push_back(std::move(p));
     }
@@ -306,7 +307,6 @@ class bulk_communication_object
         static_assert(std::is_same_v<std::decay_t<decltype(bi.field->desc())>, ghx_field_desc>,
                       "bulk (zero-copy) exchange is implemented for structured fields");
         if (m_init) throw std::runtime_error("this bulk communication object has been initialized already");
-        if (m_fields.size() == GHX_MAX_SLOTS) throw std::runtime_error("at most 64 fields per bulk object");
         local_field f{bi.pattern, bi.local_index, bi.field->desc(),
                       const_cast<void*>(static_cast<const void*>(bi.field->data())), int(bi.field->domain_id()), 0};
         for (const auto& g : m_fields) f.j += g.domain == f.domain;
@@ -413,26 +413,31 @@ class bulk_communication_object
                 ptr_of[m.target] = ptr;
             }
         }
-        // put plans of <= 64 messages and <= 64 target fields
+        // put plans (one launch each) of <= 64 messages, <= 64 source and <= 64 target fields
         std::vector<msg> chunk;
+        std::vector<int> srcs;
         std::vector<std::pair<int, int>> dsts;
         for (std::size_t i = 0; i <= msgs.size(); ++i)
         {
             const bool end = i == msgs.size();
-            const bool full = !end && (chunk.size() == GHX_MAX_SLOTS ||
-                                       (std::find(dsts.begin(), dsts.end(), msgs[i].target) == dsts.end() &&
-                                        dsts.size() == GHX_MAX_SLOTS));
+            const bool full =
+                !end && (chunk.size() == GHX_MAX_SLOTS ||
+                         (std::find(srcs.begin(), srcs.end(), msgs[i].src) == srcs.end() &&
+                          srcs.size() == GHX_MAX_SLOTS) ||
+                         (std::find(dsts.begin(), dsts.end(), msgs[i].target) == dsts.end() &&
+                          dsts.size() == GHX_MAX_SLOTS));
             if ((end || full) && !chunk.empty())
             {
-                make_put(chunk, dsts, all, ptr_of);
+                make_put(chunk, srcs, dsts, all, ptr_of);
                 chunk.clear();
+                srcs.clear();
                 dsts.clear();
             }
             if (end) break;
+            if (std::find(srcs.begin(), srcs.end(), msgs[i].src) == srcs.end()) srcs.push_back(msgs[i].src);
             if (std::find(dsts.begin(), dsts.end(), msgs[i].target) == dsts.end()) dsts.push_back(msgs[i].target);
             chunk.push_back(std::move(msgs[i]));
         }
-        for (const auto& f : m_fields) m_src.push_back(f.data);
         m_init = true;
     }
 
@@ -453,7 +458,7 @@ class bulk_communication_object
             else check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
             check_ghx(ghx_epochs_enqueue(m_ep, 0, m_stream), "ghx_epochs_enqueue(open)");
             for (auto& p : m_puts)
-                check_ghx(ghx_put_execute(p.h, m_src.data(), std::int32_t(m_src.size()), p.dst.data(),
+                check_ghx(ghx_put_execute(p.h, p.src.data(), std::int32_t(p.src.size()), p.dst.data(),
                                           std::int32_t(p.dst.size()), m_stream),
                           "ghx_put_execute");
             check_ghx(ghx_epochs_enqueue(m_ep, 1, m_stream), "ghx_epochs_enqueue(close)");
@@ -465,7 +470,7 @@ class bulk_communication_object
         else check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
         barrier();  // every target open
         for (auto& p : m_puts)
-            check_ghx(ghx_put_execute(p.h, m_src.data(), std::int32_t(m_src.size()), p.dst.data(),
+            check_ghx(ghx_put_execute(p.h, p.src.data(), std::int32_t(p.src.size()), p.dst.data(),
                                       std::int32_t(p.dst.size()), m_stream),
                       "ghx_put_execute");
         check_hip(hipStreamSynchronize(m_stream), "hipStreamSynchronize");

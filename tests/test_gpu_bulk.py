@@ -106,3 +106,34 @@ def test_put_rejects_mismatched_sides():
     rc = _ghx.lib().ghx_put_create(ctypes.byref(entries[0][0]), 1, ctypes.byref(entries[1][0]),
                                    1, ctypes.byref(h))
     assert rc == -1 and b"same message bytes" in _ghx.lib().ghx_last_error()
+
+
+def test_bulk_more_fields_than_one_launch_holds():
+    """70 fields of one periodic domain in one bulk object: the puts are planned in launches of
+    <= 64 source and <= 64 target fields (ghx_put_create takes one launch's worth), every halo
+    equal to the oracle's exchange."""
+    from ghex_amd import make_context, make_bulk_communication_object
+    from ghex_amd.structured import regular as R
+    from tests.gpu_util import device_field
+    N, Hw = 6, 1
+    E = N + 2 * Hw
+    ranks, gf, gl = H.cube_domains(N, (1, 1, 1))
+    dom = ranks[0][0]
+    ctx = make_context()
+    dd = R.DomainDescriptor(0, dom.first, dom.last)
+    pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (True,) * 3), [dd])
+    opat = orc.regular_make_pattern(ranks, gf, gl, (Hw,) * 6, (1, 1, 1))
+    bco = make_bulk_communication_object(ctx)
+    pairs, rf = [], []
+    for k in range(70):
+        a, spec = H.linear_index_field(dom, N, Hw, gl, seed=k)
+        base, logical = device_field(a.copy(), (2, 1, 0))
+        bco.add_field(pc(R.make_field_descriptor(dd, logical, (Hw,) * 3, (E,) * 3)))
+        pairs.append((base, a))
+        rf.append((spec, 0, 0, 0))
+    bco.init()
+    assert bco.bytes_per_exchange() == 70 * (E ** 3 - N ** 3) * 8
+    bco.exchange().wait()
+    orc.regular_exchange([rf], {0: opat}, 1)
+    for base, a in pairs:
+        np.testing.assert_array_equal(base.cpu().numpy(), a)
