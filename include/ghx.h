@@ -415,7 +415,8 @@ int ghx_ipc_close(void* base);
  * iteration spaces of a sender's send halo (its local coordinates, its field) and of the
  * receiver's recv halo for the same key (the receiver's coordinates and field), each entry's
  * buffer_slot/buffer_offset placing it in a virtual message exactly as ghx_plan_create would.
- * Field slots: src entries index src_fields, dst entries index dst_fields (<= 64 each).
+ * Field slots: src entries index src_fields, dst entries index dst_fields (< 64 each: one
+ * launch; the bulk objects group their messages into several put plans).
  * Execution copies every element straight from the source field into the target field (peer
  * memory through ghx_ipc_import, or the same device): no buffer, one launch. Fails with
  * GHX_ERR_INVALID when the two sides do not describe the same bytes. */
