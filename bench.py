@@ -703,6 +703,8 @@ def extras(args, torch, dist, dev, stream, out, v):
                                                (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
         del a, b
         torch.cuda.empty_cache()
+        if world == 1:
+            roof["read_floor"] = pack_read_floor(N, Hw, roof)
 
     if world == 1:
         # the other BASELINE configs, per GPU (their 8-GPU forms are weak-scaled copies)
@@ -718,6 +720,40 @@ def extras(args, torch, dist, dev, stream, out, v):
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, Hw, args.cpu_seconds)
+
+
+def pack_read_floor(N, Hw, roof):
+    """The pack's address-set floor on this box (developer measurement, tools/pack_floor.hip via
+    tools/lib/libpackfloor.so): a kernel that does nothing but load one 16-B vector
+    from each 128-B field line the pack must read (x-face lines first, as the pack dispatches
+    them) and stream the buffer writes, timed like pack_kernel_us (the kernel's own begin/end
+    events, medians). pack_vs_floor = floor / pack: the share of the bare memory-system time the
+    pack kernel achieves."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "lib", "libpackfloor.so")
+    if not os.path.exists(path):
+        return {"error": "tools/lib/libpackfloor.so not built (make -C tools)"}
+    try:
+        L = ctypes.CDLL(path)
+        L.ghx_probe_pack_floor.restype = ctypes.c_int
+        L.ghx_probe_pack_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_int64)]
+        us = (ctypes.c_double * 8)()
+        c = (ctypes.c_int64 * 3)()
+        rc = L.ghx_probe_pack_floor(N, Hw, 21, us, c)
+    except Exception as e:  # reported, never fatal
+        return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+    if rc:
+        return {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
+    floor = us[6]
+    return {"xface_lines": c[0], "long_lines": c[1],
+            "xface_only_us": round(us[0], 2), "long_only_us": round(us[2], 2),
+            "reads_us": round(us[4], 2), "reads_writes_us": round(floor, 2),
+            "reads_writes_cold_us": round(us[7], 2),
+            "pack_kernel_us": roof.get("pack_kernel_us"),
+            "pack_vs_floor": round(floor / roof["pack_kernel_us"], 3)
+            if roof.get("pack_kernel_us") else None}
 
 
 def host_staged(torch, dev, co, plan, send, recv, pack, unpack, timed, step_bytes, n_halo, k):

@@ -1,0 +1,196 @@
+// pack_floor.hip — developer measurement (not product): the read floor of the 512^3 H=2 pack.
+// Builds, on the host, the exact set of 128-B field lines the pack must read (the 26 send boxes
+// of one periodic 516^3 fp64 domain: every row's byte range -> the lines it touches, deduped),
+// split into the x-face class (lines touched by rows of <= H cells: x faces, x edges, corners)
+// and the long-row class (the rest), and times a kernel that does nothing but load ONE 16-B
+// vector from each listed line (lane-linear over the list, 4 loads in flight per lane, no index
+// math, no writes). That is the least the memory system can take to deliver the pack's reads in
+// that class order, whatever a pack kernel does; the pack's own time is measured beside it by
+// bench.py / tools/microbench.py on the same box.
+//   xface    the x-face lines alone
+//   long     the long-row lines alone
+//   both     x-face lines first, then long-row lines, one launch (the pack's dispatch order)
+//   both_rw  as both, plus the pack's buffer writes (25.4 MB, 16 B per lane, streamed by the
+//            same grid after its loads)
+// Warm (footprint resident in the 256 MiB Infinity Cache, as in the bench's back-to-back steps)
+// and cold (right after a 1 GiB read-only sweep: nothing dirty to write back). Each launch timed
+// by its own begin/end events (hipExtLaunchKernelGGL: the interval a rocprofv3 kernel trace
+// reports, as bench.py's pack_kernel_us), median of `reps`.
+// Built by tools/Makefile (from __graft_entry__.build()) as tools/bin/pack_floor (one JSON line
+// per measurement) and tools/lib/libpackfloor.so (ghx_probe_pack_floor, called by bench.py).
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <vector>
+
+#define CK(x)                   \
+    do                          \
+    {                           \
+        if ((x) != hipSuccess)  \
+        {                       \
+            rc = __LINE__;      \
+            goto done;          \
+        }                       \
+    } while (0)
+
+using v4 = unsigned __attribute__((ext_vector_type(4)));
+constexpr int kU = 4;
+
+// lines[0, n): one 16-B load per line; optionally the grid then streams `wbytes` of writes
+__global__ __launch_bounds__(256) void k_lines(const uint32_t* __restrict__ lines, uint32_t n,
+                                               const char* __restrict__ field, v4* __restrict__ buf,
+                                               uint64_t wvec, unsigned* sink)
+{
+    v4 acc{0, 0, 0, 0};
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t base = blockIdx.x * 256u + threadIdx.x; base < n; base += kU * stride)
+    {
+        uint32_t l[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) l[u] = base + u * stride < n ? lines[base + u * stride] : 0xffffffffu;
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (l[u] != 0xffffffffu) acc ^= *(const v4*)(field + uint64_t(l[u]) * 128);
+    }
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < wvec; i += uint64_t(stride))
+        buf[i] = v4{unsigned(i), 1, 2, 3};
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
+}
+
+__global__ __launch_bounds__(256) void k_sweep(const v4* p, size_t n, unsigned* sink)
+{
+    v4 acc{0, 0, 0, 0};
+    for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += size_t(gridDim.x) * 256) acc ^= p[i];
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
+}
+
+// The 26 send boxes of one periodic (N+2H)^3 fp64 domain: the 128-B lines their rows touch,
+// x-face class (rows of <= H cells) first; useful = the pack's algorithmic read bytes.
+static void line_sets(int N, int H, std::vector<uint32_t>& xf, std::vector<uint32_t>& lg, uint64_t& useful)
+{
+    const int E = N + 2 * H;
+    const uint64_t pitch = uint64_t(E) * 8, plane = pitch * E;
+    std::vector<uint8_t> cls(size_t(plane * E / 128 + 1), 0);  // 1 x-face, 2 long
+    useful = 0;
+    const int lo[3] = {H, H, N};  // dir -1, 0, +1: first interior coordinate of the box
+    const int hi[3] = {2 * H - 1, N + H - 1, N + H - 1};
+    for (int dz = 0; dz < 3; ++dz)
+        for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx)
+            {
+                if (dx == 1 && dy == 1 && dz == 1) continue;
+                const int x0 = lo[dx], x1 = hi[dx];
+                const bool shortrow = x1 - x0 + 1 <= H;
+                for (int z = lo[dz]; z <= hi[dz]; ++z)
+                    for (int y = lo[dy]; y <= hi[dy]; ++y)
+                    {
+                        const uint64_t b = uint64_t(z) * plane + uint64_t(y) * pitch + uint64_t(x0) * 8;
+                        const uint64_t e = b + uint64_t(x1 - x0 + 1) * 8;
+                        useful += e - b;
+                        for (uint64_t l = b / 128; l <= (e - 1) / 128; ++l)
+                            if (shortrow) cls[l] = 1;
+                            else if (!cls[l]) cls[l] = 2;
+                    }
+            }
+    for (size_t l = 0; l < cls.size(); ++l)
+        if (cls[l] == 1) xf.push_back(uint32_t(l));
+        else if (cls[l] == 2) lg.push_back(uint32_t(l));
+}
+
+// out_us[8]: {xface, long, both, both_rw} x {warm, cold} (microseconds, kernel-own events);
+// counts[3]: x-face lines, long-row lines, useful bytes. Returns 0, or the failing source line.
+extern "C" int ghx_probe_pack_floor(int N, int H, int reps, double* out_us, int64_t* counts)
+{
+    int rc = 0;
+    std::vector<uint32_t> xf, lg;
+    uint64_t useful = 0;
+    line_sets(N, H, xf, lg, useful);
+    std::vector<uint32_t> both(xf);
+    both.insert(both.end(), lg.begin(), lg.end());
+    const int E = N + 2 * H;
+    const size_t fbytes = size_t(E) * E * E * 8, flush_bytes = size_t(1) << 30;
+    char *field = nullptr, *fl = nullptr;
+    v4* buf = nullptr;
+    unsigned* sink = nullptr;
+    uint32_t *d_xf = nullptr, *d_lg = nullptr, *d_both = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const int grid = 256 * 8;
+    counts[0] = int64_t(xf.size());
+    counts[1] = int64_t(lg.size());
+    counts[2] = int64_t(useful);
+    CK(hipMalloc(&field, fbytes));
+    CK(hipMalloc(&fl, flush_bytes));
+    CK(hipMalloc(&buf, useful + 64));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMalloc(&d_xf, xf.size() * 4 + 4));
+    CK(hipMalloc(&d_lg, lg.size() * 4 + 4));
+    CK(hipMalloc(&d_both, both.size() * 4 + 4));
+    CK(hipMemcpy(d_xf, xf.data(), xf.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_lg, lg.data(), lg.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_both, both.data(), both.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(field, 1, fbytes));
+    CK(hipMemset(fl, 2, flush_bytes));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    {
+        const uint32_t* lists[4] = {d_xf, d_lg, d_both, d_both};
+        const size_t ns[4] = {xf.size(), lg.size(), both.size(), both.size()};
+        const uint64_t wv[4] = {0, 0, 0, useful / 16};
+        for (int j = 0; j < 4; ++j)
+            for (int cold = 0; cold < 2; ++cold)
+            {
+                std::vector<float> t;
+                for (int i = 0; i < reps; ++i)
+                {
+                    if (cold)
+                        hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, 0, (const v4*)fl,
+                                           flush_bytes / 16, sink);
+                    else
+                        hipLaunchKernelGGL(k_lines, dim3(grid), dim3(256), 0, 0, lists[j], uint32_t(ns[j]),
+                                           (const char*)field, buf, wv[j], sink);
+                    hipExtLaunchKernelGGL(k_lines, dim3(grid), dim3(256), 0, 0, e0, e1, 0, lists[j],
+                                          uint32_t(ns[j]), (const char*)field, buf, wv[j], sink);
+                    CK(hipEventSynchronize(e1));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    t.push_back(ms * 1e3f);
+                }
+                std::sort(t.begin(), t.end());
+                out_us[2 * j + cold] = t[t.size() / 2];
+            }
+    }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    for (void* p : {(void*)field, (void*)fl, (void*)buf, (void*)sink, (void*)d_xf, (void*)d_lg, (void*)d_both})
+        if (p) (void)hipFree(p);
+    return rc;
+}
+
+#ifdef PACK_FLOOR_MAIN
+int main(int argc, char** argv)
+{
+    const int reps = argc > 1 ? atoi(argv[1]) : 21;
+    const int N = argc > 2 ? atoi(argv[2]) : 512, H = argc > 3 ? atoi(argv[3]) : 2;
+    double us[8];
+    int64_t c[3];
+    const int rc = ghx_probe_pack_floor(N, H, reps, us, c);
+    if (rc)
+    {
+        printf("{\"error\": \"HIP call failed at pack_floor.hip:%d\"}\n", rc);
+        return 1;
+    }
+    printf("{\"config\": \"%d^3 fp64 H=%d pack read set\", \"useful_bytes\": %lld, \"xface_lines\": %lld, "
+           "\"long_lines\": %lld}\n", N, H, (long long)c[2], (long long)c[0], (long long)c[1]);
+    const char* names[4] = {"xface", "long", "both", "both_rw"};
+    for (int j = 0; j < 4; ++j)
+        for (int cold = 0; cold < 2; ++cold)
+            printf("{\"set\": \"%s\", \"cold\": %d, \"us\": %.2f}\n", names[j], cold, us[2 * j + cold]);
+    return 0;
+}
+#endif
