@@ -537,7 +537,8 @@ int ghx_tune(const char* key, int32_t value)
         }
         else if (k == "small_tile_rows")
         {
-            if (value < 64 || value > (1 << 16)) throw invalid("small_tile_rows must be in [64, 65536]");
+            if (value != 0 && (value < 64 || value > (1 << 16)))
+                throw invalid("small_tile_rows must be 0 (auto) or in [64, 65536]");
             g_tune.small_tile_rows = uint32_t(value);
         }
         else if (k == "grid_cap")

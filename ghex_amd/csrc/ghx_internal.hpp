@@ -35,7 +35,8 @@ struct tuning
                                        // interleaved A/B runs with register forwarding:
                                        // H=2 8 KiB 26.4 vs 4 KiB 27.9 us; H=1 18.6 vs 19.9;
                                        // H=3 32.8 vs 32.0 (profiles/r01c_fwd_tile_ab.jsonl)
-    uint32_t small_tile_rows = 4096;   // rows per tile of segments with short rows
+    uint32_t small_tile_rows = 0;      // rows per tile of segments with short rows (0: by the
+                                       // plan's short-row count, ghx_plan.cpp short_tile_rows)
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
     int order = 1;                     // tile dispatch order: 0 segment order, 1 short-row

@@ -61,12 +61,25 @@ std::vector<int32_t> line_partners(const std::vector<seg_u>& segs)
     return std::vector<int32_t>(segs.size(), -1);
 }
 
-// Rows per tile of a short-row segment: structured short rows want few large tiles (measured
-// best: 4096 rows); index-list gathers are latency-bound random accesses and want many
-// workgroups in flight (512 rows), except run-heavy lists on the run path, which stream
-// (2048 rows: tools/urun_bench.py, contiguous lids 40 -> 33 us).
-uint32_t short_tile_rows(const seg_s&) { return g_tune.small_tile_rows; }
-uint32_t short_tile_rows(const seg_u& s)
+// Rows per tile of a short-row segment. Structured short rows (x-normal faces, edges, corners
+// of a unit-stride field) are request-bound: a plan's R short rows are cut so that they make
+// about R/128 tiles when each row is one 16-B lane access (16-B rows: H=2 fp64), R/256 otherwise,
+// a power of two in [512, 4096] (knob small_tile_rows > 0 overrides). Measured with the
+// graph-timed two-launch step over N = 256..640 and H = 1..3 (profiles/r03_tile_rows_sweep.jsonl,
+// DESIGN §4): a fixed 4096 rows — the round-1 choice, made at 512^3 H=2 where it still wins — left
+// small cubes with a few dozen x-face workgroups (256^3 H=3: 35.4 us vs 14.9 us at 1024 rows) and
+// was 15-17 % slower at 512^3 H=1/H=3 than 2048 rows. Index-list gathers are latency-bound
+// random accesses and want many workgroups in flight (512 rows), except run-heavy lists on the
+// run path, which stream (2048 rows: tools/urun_bench.py, contiguous lids 40 -> 33 us).
+uint32_t short_tile_rows(const seg_s& s, uint64_t short_rows)
+{
+    if (g_tune.small_tile_rows) return g_tune.small_tile_rows;
+    const uint64_t want = short_rows / (s.row_bytes == 16 ? 128 : 256);
+    uint32_t r = 512;
+    while (r < 4096 && uint64_t(r) * 2 <= want) r *= 2;
+    return r;
+}
+uint32_t short_tile_rows(const seg_u& s, uint64_t)
 {
     return s.runs == 2 ? g_tune.u_run_tile_rows : g_tune.u_tile_rows;
 }
@@ -78,15 +91,16 @@ template<typename Seg>
 std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
 {
     std::vector<std::vector<uint32_t>> per(segs.size());
+    uint64_t short_rows = 0;  // the plan's short rows (one launch's request-bound work)
+    for (const auto& sg : segs)
+        if (sg.row_bytes < g_tune.small_row_bytes) short_rows += sg.bytes / sg.row_bytes;
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
         const bool small = segs[i].row_bytes < g_tune.small_row_bytes;
         uint32_t tb = g_tune.tile_bytes;
         if (small)
         {
-            // structured short rows: few large tiles (measured best: 4096 rows); index-list
-            // gathers are latency-bound random accesses and want many workgroups in flight
-            const uint32_t rows = short_tile_rows(segs[i]);
+            const uint32_t rows = short_tile_rows(segs[i], short_rows);
             const uint64_t want = uint64_t(rows) * segs[i].row_bytes;
             tb = uint32_t(std::max<uint64_t>(segs[i].row_bytes, std::min<uint64_t>(want, kMaxTileBytes)));
             tb -= tb % segs[i].row_bytes;  // whole rows per tile

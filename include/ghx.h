@@ -46,7 +46,8 @@ typedef void* ghx_stream;
 
 /* Process-wide tuning knobs (development / benchmarking; defaults are the measured best):
  * "grid_cap" (max workgroups, 0 = one per tile), "tile_bytes" (buffer bytes per workgroup tile),
- * "small_tile_rows" (rows per tile of short-row structured segments), "small_row_bytes" (rows
+ * "small_tile_rows" (rows per tile of short-row structured segments; 0 = by the plan's count of
+ * short rows, the default), "small_row_bytes" (rows
  * shorter than this are "short"), "order" (0 segment order, 1 short-row segments first),
  * "xcd_pair" (0|1: line-sharing short-row segment pairs dispatched in lock-step groups of 8
  * tiles, same XCD), "short_pol" (field-side cache policy of short-row segments: bit 0
