@@ -401,12 +401,12 @@ uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, cons
         s.bytes = uint32_t(rows * L);
         s.mag_row = make_magic(uint32_t(L));
         for (int k = 0; k < 3; ++k) s.mag_ext[k] = make_magic(s.ext[k]);
-        int w = wlog2_of(uint64_t(L));
-        w = std::min(w, wlog2_of(uint64_t(s.field_off)));
-        w = std::min(w, wlog2_of(s.buf_off));
+        const int wb = std::min(wlog2_of(uint64_t(L)), wlog2_of(s.buf_off));  // buffer side
+        int wf = wlog2_of(uint64_t(s.field_off));                             // field side
         for (int k = 0; k < n_outer; ++k)
-            if (s.ext[k] > 1) w = std::min(w, wlog2_of(uint64_t(s.stride[k] < 0 ? -s.stride[k] : s.stride[k])));
-        s.wlog2 = uint8_t(w);
+            if (s.ext[k] > 1) wf = std::min(wf, wlog2_of(uint64_t(s.stride[k] < 0 ? -s.stride[k] : s.stride[k])));
+        s.wlog2 = uint8_t(std::min(wb, wf));
+        s.u16 = uint8_t(g_tune.field_unaligned16 && wb == 4 && wf >= 2 && wf < 4);
         out.push_back(s);
     }
     return uint64_t(n * elem);
