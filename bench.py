@@ -722,38 +722,59 @@ def extras(args, torch, dist, dev, stream, out, v):
         out["cpu_baseline"] = cpu_baseline(N, Hw, args.cpu_seconds)
 
 
-def pack_read_floor(N, Hw, roof):
-    """The pack's address-set floor on this box (developer measurement, tools/pack_floor.hip via
-    tools/lib/libpackfloor.so): a kernel that does nothing but load one 16-B vector
-    from each 128-B field line the pack must read (x-face lines first, as the pack dispatches
-    them) and stream the buffer writes, timed like pack_kernel_us (the kernel's own begin/end
-    events, medians). pack_vs_floor = floor / pack: the share of the bare memory-system time the
-    pack kernel achieves."""
+def _floor_lib():
     import ctypes
     path = os.path.join(ROOT, "tools", "lib", "libpackfloor.so")
     if not os.path.exists(path):
-        return {"error": "tools/lib/libpackfloor.so not built (make -C tools)"}
+        return None
+    L = ctypes.CDLL(path)
+    for name in ("ghx_probe_pack_floor", "ghx_probe_unpack_floor"):
+        f = getattr(L, name)
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                      ctypes.POINTER(ctypes.c_int64)]
+    return L
+
+
+def pack_read_floor(N, Hw, roof):
+    """The launches' address-set floors on this box (developer measurement, tools/pack_floor.hip
+    via tools/lib/libpackfloor.so). Pack: a kernel that does nothing but load one
+    16-B vector from each 128-B field line the pack must read (x-face lines first, as the pack
+    dispatches them) and stream the buffer writes. Unpack ("write_floor"): a kernel that streams
+    the buffer in and writes each halo row's bytes once (16-B pieces where aligned). Timed like
+    pack_kernel_us (the kernel's own begin/end events, medians); *_vs_floor = floor / kernel."""
+    import ctypes
     try:
-        L = ctypes.CDLL(path)
-        L.ghx_probe_pack_floor.restype = ctypes.c_int
-        L.ghx_probe_pack_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                           ctypes.POINTER(ctypes.c_double),
-                                           ctypes.POINTER(ctypes.c_int64)]
+        L = _floor_lib()
+        if L is None:
+            return {"error": "tools/lib/libpackfloor.so not built (make -C tools)"}
         us = (ctypes.c_double * 8)()
         c = (ctypes.c_int64 * 3)()
         rc = L.ghx_probe_pack_floor(N, Hw, 21, us, c)
+        if rc:
+            return {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
+        out = {"xface_lines": c[0], "long_lines": c[1],
+               "xface_only_us": round(us[0], 2), "long_only_us": round(us[2], 2),
+               "reads_us": round(us[4], 2), "reads_writes_us": round(us[6], 2),
+               "reads_writes_cold_us": round(us[7], 2),
+               "pack_kernel_us": roof.get("pack_kernel_us"),
+               "pack_vs_floor": round(us[6] / roof["pack_kernel_us"], 3)
+               if roof.get("pack_kernel_us") else None}
+        rc = L.ghx_probe_unpack_floor(N, Hw, 21, us, c)
+        if rc:
+            out["write_floor"] = {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
+        else:
+            out["write_floor"] = {
+                "xface_pieces": c[0], "long_pieces": c[1],
+                "xface_writes_us": round(us[0], 2), "long_writes_us": round(us[2], 2),
+                "writes_us": round(us[4], 2), "writes_reads_us": round(us[6], 2),
+                "writes_reads_cold_us": round(us[7], 2),
+                "unpack_kernel_us": roof.get("unpack_kernel_us"),
+                "unpack_vs_floor": round(us[6] / roof["unpack_kernel_us"], 3)
+                if roof.get("unpack_kernel_us") else None}
+        return out
     except Exception as e:  # reported, never fatal
         return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
-    if rc:
-        return {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
-    floor = us[6]
-    return {"xface_lines": c[0], "long_lines": c[1],
-            "xface_only_us": round(us[0], 2), "long_only_us": round(us[2], 2),
-            "reads_us": round(us[4], 2), "reads_writes_us": round(floor, 2),
-            "reads_writes_cold_us": round(us[7], 2),
-            "pack_kernel_us": roof.get("pack_kernel_us"),
-            "pack_vs_floor": round(floor / roof["pack_kernel_us"], 3)
-            if roof.get("pack_kernel_us") else None}
 
 
 def host_staged(torch, dev, co, plan, send, recv, pack, unpack, timed, step_bytes, n_halo, k):

@@ -1,4 +1,6 @@
-// pack_floor.hip — developer measurement (not product): the read floor of the 512^3 H=2 pack.
+// pack_floor.hip — developer measurement (not product): the read floor of the 512^3 H=2 pack,
+// and the write floor of the unpack (ghx_probe_unpack_floor: the halo rows' bytes written once,
+// 16-B pieces where aligned, plus the buffer stream read).
 // Builds, on the host, the exact set of 128-B field lines the pack must read (the 26 send boxes
 // of one periodic 516^3 fp64 domain: every row's byte range -> the lines it touches, deduped),
 // split into the x-face class (lines touched by rows of <= H cells: x faces, x edges, corners)
@@ -62,6 +64,30 @@ __global__ __launch_bounds__(256) void k_lines(const uint32_t* __restrict__ line
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
 }
 
+// The unpack's mirror: the grid streams `rvec` vectors of the buffer in, then writes each listed
+// halo piece (bit 31: 16 B, else 8 B; bits 0-30: byte address / 8) once.
+__global__ __launch_bounds__(256) void k_pieces(const uint32_t* __restrict__ pieces, uint32_t n,
+                                                char* __restrict__ field, const v4* __restrict__ buf,
+                                                uint64_t rvec, unsigned* sink)
+{
+    v4 acc{0, 0, 0, 0};
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < rvec; i += uint64_t(stride)) acc ^= buf[i];
+    for (uint32_t base = blockIdx.x * 256u + threadIdx.x; base < n; base += kU * stride)
+    {
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+        {
+            if (base + u * stride >= n) break;
+            const uint32_t q = pieces[base + u * stride];
+            char* a = field + uint64_t(q & 0x7fffffffu) * 8;
+            if (q >> 31) *(v4*)a = v4{q, acc.x, 2, 3};
+            else *(unsigned __attribute__((ext_vector_type(2)))*)a = {q, acc.y};
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
+}
+
 __global__ __launch_bounds__(256) void k_sweep(const v4* p, size_t n, unsigned* sink)
 {
     v4 acc{0, 0, 0, 0};
@@ -100,6 +126,112 @@ static void line_sets(int N, int H, std::vector<uint32_t>& xf, std::vector<uint3
     for (size_t l = 0; l < cls.size(); ++l)
         if (cls[l] == 1) xf.push_back(uint32_t(l));
         else if (cls[l] == 2) lg.push_back(uint32_t(l));
+}
+
+// The 26 receive boxes (halos) of the same domain as write pieces: each row's byte range in
+// 16-B pieces where 16-B aligned, 8-B pieces at the edges; x-face class first.
+static void piece_sets(int N, int H, std::vector<uint32_t>& xf, std::vector<uint32_t>& lg, uint64_t& useful)
+{
+    const int E = N + 2 * H;
+    const uint64_t pitch = uint64_t(E) * 8, plane = pitch * E;
+    useful = 0;
+    const int lo[3] = {0, H, N + H};  // dir -1, 0, +1: first halo-box coordinate
+    const int hi[3] = {H - 1, N + H - 1, N + 2 * H - 1};
+    for (int dz = 0; dz < 3; ++dz)
+        for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx)
+            {
+                if (dx == 1 && dy == 1 && dz == 1) continue;
+                const int x0 = lo[dx], x1 = hi[dx];
+                auto& out = x1 - x0 + 1 <= H ? xf : lg;
+                for (int z = lo[dz]; z <= hi[dz]; ++z)
+                    for (int y = lo[dy]; y <= hi[dy]; ++y)
+                    {
+                        uint64_t b = uint64_t(z) * plane + uint64_t(y) * pitch + uint64_t(x0) * 8;
+                        const uint64_t e = b + uint64_t(x1 - x0 + 1) * 8;
+                        useful += e - b;
+                        while (b < e)
+                        {
+                            const bool w16 = b % 16 == 0 && e - b >= 16;
+                            out.push_back(uint32_t(b / 8) | (w16 ? 0x80000000u : 0u));
+                            b += w16 ? 16 : 8;
+                        }
+                    }
+            }
+    std::sort(xf.begin(), xf.end(), [](uint32_t a, uint32_t b) { return (a & 0x7fffffffu) < (b & 0x7fffffffu); });
+    std::sort(lg.begin(), lg.end(), [](uint32_t a, uint32_t b) { return (a & 0x7fffffffu) < (b & 0x7fffffffu); });
+}
+
+// out_us[8]: {xface, long, both, both + buffer reads} x {warm, cold} of the unpack's halo writes;
+// counts[3]: x-face pieces, long-row pieces, useful bytes. Returns 0, or the failing source line.
+extern "C" int ghx_probe_unpack_floor(int N, int H, int reps, double* out_us, int64_t* counts)
+{
+    int rc = 0;
+    std::vector<uint32_t> xf, lg;
+    uint64_t useful = 0;
+    piece_sets(N, H, xf, lg, useful);
+    std::vector<uint32_t> both(xf);
+    both.insert(both.end(), lg.begin(), lg.end());
+    const int E = N + 2 * H;
+    const size_t fbytes = size_t(E) * E * E * 8, flush_bytes = size_t(1) << 30;
+    char *field = nullptr, *fl = nullptr;
+    v4* buf = nullptr;
+    unsigned* sink = nullptr;
+    uint32_t *d_xf = nullptr, *d_lg = nullptr, *d_both = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const int grid = 256 * 8;
+    counts[0] = int64_t(xf.size());
+    counts[1] = int64_t(lg.size());
+    counts[2] = int64_t(useful);
+    if (fbytes / 8 >= (size_t(1) << 31)) return __LINE__;  // piece addresses are 31-bit / 8
+    CK(hipMalloc(&field, fbytes));
+    CK(hipMalloc(&fl, flush_bytes));
+    CK(hipMalloc(&buf, useful + 64));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMalloc(&d_xf, xf.size() * 4 + 4));
+    CK(hipMalloc(&d_lg, lg.size() * 4 + 4));
+    CK(hipMalloc(&d_both, both.size() * 4 + 4));
+    CK(hipMemcpy(d_xf, xf.data(), xf.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_lg, lg.data(), lg.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_both, both.data(), both.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(field, 1, fbytes));
+    CK(hipMemset(buf, 3, useful + 64));
+    CK(hipMemset(fl, 2, flush_bytes));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    {
+        const uint32_t* lists[4] = {d_xf, d_lg, d_both, d_both};
+        const size_t ns[4] = {xf.size(), lg.size(), both.size(), both.size()};
+        const uint64_t rv[4] = {0, 0, 0, useful / 16};
+        for (int j = 0; j < 4; ++j)
+            for (int cold = 0; cold < 2; ++cold)
+            {
+                std::vector<float> t;
+                for (int i = 0; i < reps; ++i)
+                {
+                    if (cold)
+                        hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, 0, (const v4*)fl,
+                                           flush_bytes / 16, sink);
+                    else
+                        hipLaunchKernelGGL(k_pieces, dim3(grid), dim3(256), 0, 0, lists[j], uint32_t(ns[j]),
+                                           field, (const v4*)buf, rv[j], sink);
+                    hipExtLaunchKernelGGL(k_pieces, dim3(grid), dim3(256), 0, 0, e0, e1, 0, lists[j],
+                                          uint32_t(ns[j]), field, (const v4*)buf, rv[j], sink);
+                    CK(hipEventSynchronize(e1));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    t.push_back(ms * 1e3f);
+                }
+                std::sort(t.begin(), t.end());
+                out_us[2 * j + cold] = t[t.size() / 2];
+            }
+    }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    for (void* p : {(void*)field, (void*)fl, (void*)buf, (void*)sink, (void*)d_xf, (void*)d_lg, (void*)d_both})
+        if (p) (void)hipFree(p);
+    return rc;
 }
 
 // out_us[8]: {xface, long, both, both_rw} x {warm, cold} (microseconds, kernel-own events);
@@ -191,6 +323,18 @@ int main(int argc, char** argv)
     for (int j = 0; j < 4; ++j)
         for (int cold = 0; cold < 2; ++cold)
             printf("{\"set\": \"%s\", \"cold\": %d, \"us\": %.2f}\n", names[j], cold, us[2 * j + cold]);
+    const int rc2 = ghx_probe_unpack_floor(N, H, reps, us, c);
+    if (rc2)
+    {
+        printf("{\"error\": \"HIP call failed at pack_floor.hip:%d\"}\n", rc2);
+        return 1;
+    }
+    printf("{\"config\": \"%d^3 fp64 H=%d unpack write set\", \"useful_bytes\": %lld, \"xface_pieces\": %lld, "
+           "\"long_pieces\": %lld}\n", N, H, (long long)c[2], (long long)c[0], (long long)c[1]);
+    const char* unames[4] = {"xface_writes", "long_writes", "writes", "writes_plus_buffer_reads"};
+    for (int j = 0; j < 4; ++j)
+        for (int cold = 0; cold < 2; ++cold)
+            printf("{\"set\": \"%s\", \"cold\": %d, \"us\": %.2f}\n", unames[j], cold, us[2 * j + cold]);
     return 0;
 }
 #endif
