@@ -535,11 +535,6 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 1) throw invalid("small_row_bytes must be >= 1");
             g_tune.small_row_bytes = uint32_t(value);
         }
-        else if (k == "field_unaligned16")
-        {
-            if (value < 0 || value > 1) throw invalid("field_unaligned16 must be 0 or 1");
-            g_tune.field_unaligned16 = value;
-        }
         else if (k == "small_tile_rows")
         {
             if (value != 0 && (value < 64 || value > (1 << 16)))

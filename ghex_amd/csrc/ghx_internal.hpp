@@ -35,7 +35,6 @@ struct tuning
                                        // interleaved A/B runs with register forwarding:
                                        // H=2 8 KiB 26.4 vs 4 KiB 27.9 us; H=1 18.6 vs 19.9;
                                        // H=3 32.8 vs 32.0 (profiles/r01c_fwd_tile_ab.jsonl)
-    int field_unaligned16 = 0;         // seg_s::u16 planning (see there)
     uint32_t small_tile_rows = 0;      // rows per tile of segments with short rows (0: by the
                                        // plan's short-row count, ghx_plan.cpp short_tile_rows)
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
@@ -96,9 +95,7 @@ struct alignas(16) seg_s
     uint8_t wlog2;        // log2 of the widest vector (<= 16 B) that divides L, offsets, strides
     uint8_t n_outer;
     uint8_t fpol;         // field-side cache policy: bit 0 nt loads, bit 1 sc1 stores
-    uint8_t u16;          // 1: rows and buffer range allow 16-B vectors but the field side is only
-                          // 4/8-B aligned (odd halo widths, fp32 fields): k_copy may move them as
-                          // 16-B vectors with unaligned field accesses (knob field_unaligned16)
+    uint8_t pad1;
     uint32_t tile_bytes;  // this segment's tile size (a multiple of the row length or 16 KiB)
     uint8_t pad[8];
 };

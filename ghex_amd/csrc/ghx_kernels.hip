@@ -21,7 +21,6 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -208,30 +207,13 @@ __device__ __forceinline__ int64_t field_offset<seg_u>(const seg_u& s, uint32_t 
     return field_offset_u(s, p);
 }
 
-// A 16-B vector at a 4-B aligned address: the HSA runtime runs kernels in unaligned-access mode,
-// and the compiler emits global_load/store_dwordx4 for it.
-using v4_a4 = unsigned __attribute__((ext_vector_type(4), aligned(4)));
-
-template<bool FU, typename V>
-struct field_vec
-{
-    using type = V;
-};
-template<typename V>
-struct field_vec<true, V>
-{
-    using type = v4_a4;
-};
-
 // Copy one tile [start, end) of a segment. Lane-linear in buffer space: lanes of a wave touch
-// consecutive W-byte vectors of the buffer; kU independent vectors in flight per lane. FU (W = 16
-// only): the field side is 4/8-B aligned, its 16-B vectors are unaligned accesses (seg_s::u16).
-template<bool PACK, int W, typename Seg, bool FU = false>
+// consecutive W-byte vectors of the buffer; kU independent vectors in flight per lane.
+template<bool PACK, int W, typename Seg>
 __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field,
                                           char* __restrict__ buf, uint32_t start, uint32_t end)
 {
     using V = typename vec_t<W>::type;
-    using FV = typename field_vec<FU, V>::type;
     const uint32_t tid = threadIdx.x;
     const uint32_t pol = s.fpol;
     for (uint32_t base = start + tid * W; base < end; base += kU * kBlock * W)
@@ -250,12 +232,7 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
             const uint32_t p = base + u * kBlock * W;
             if (p < end)
             {
-                if constexpr (PACK && FU)
-                {
-                    const FV x = fload<FV>(field + fo[u], pol);
-                    v[u] = V{x.x, x.y, x.z, x.w};
-                }
-                else if (PACK) v[u] = fload<V>(field + fo[u], pol);
+                if (PACK) v[u] = fload<V>(field + fo[u], pol);
                 else v[u] = vload<V>(buf + p);
             }
         }
@@ -266,7 +243,6 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
             if (p < end)
             {
                 if (PACK) vstore<V>(buf + p, v[u]);
-                else if constexpr (FU) fstore<FV>(field + fo[u], FV{v[u].x, v[u].y, v[u].z, v[u].w}, pol);
                 else fstore<V>(field + fo[u], v[u], pol);
             }
         }
@@ -283,6 +259,8 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
 // the hardware skips; mixed waves execute both, masked. Field accesses of a run are only
 // L-aligned: the HSA runtime runs kernels in unaligned-access mode, so a 16-B access at a 4-B
 // aligned address is legal (split by the TA where it crosses a line).
+using v4_a4 = unsigned __attribute__((ext_vector_type(4), aligned(4)));
+
 template<int K>
 __device__ __forceinline__ void load_lids(const seg_u& s, uint32_t r0, int64_t (&l)[K])
 {
@@ -474,15 +452,6 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         int w = s.wlog2;
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
-        if constexpr (std::is_same_v<Seg, seg_s>)
-        {
-            if (s.u16 && w < 4 && ptr_wlog2(reinterpret_cast<uint64_t>(buf)) == 4 &&
-                ptr_wlog2(reinterpret_cast<uint64_t>(field)) >= 2)
-            {
-                copy_tile<PACK, 16, seg_s, true>(s, field, buf, start, end);
-                continue;
-            }
-        }
         copy_any<PACK>(s, field, buf, start, end, w);
     }
 }

@@ -406,7 +406,6 @@ uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, cons
         for (int k = 0; k < n_outer; ++k)
             if (s.ext[k] > 1) wf = std::min(wf, wlog2_of(uint64_t(s.stride[k] < 0 ? -s.stride[k] : s.stride[k])));
         s.wlog2 = uint8_t(std::min(wb, wf));
-        s.u16 = uint8_t(g_tune.field_unaligned16 && wb == 4 && wf >= 2 && wf < 4);
         out.push_back(s);
     }
     return uint64_t(n * elem);

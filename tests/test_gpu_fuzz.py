@@ -112,7 +112,6 @@ def run_case(case):
         ranks_fields.append(rf)
     obufs = orc.regular_exchange(ranks_fields, pat_o, nr)
     _ghx.call("ghx_tune", b"mixed_always", 1 if case["mixed"] else 0)
-    _ghx.call("ghx_tune", b"field_unaligned16", case["seed"] % 2)
     try:
         plans, bufs = emulated_exchange(cos, bis_all, mixed=case["mixed"])
     finally:

@@ -295,21 +295,6 @@ def test_mixed_five_fields_config4_shape():
             np.testing.assert_array_equal(bufs[r][0][i][:x["size"]].cpu().numpy()[m], ob[m])
 
 
-@pytest.mark.parametrize("u16", [0, 1])
-def test_mixed_fields_with_unaligned_field_vectors(u16):
-    """Config 4's mixed f64/f32 fields at H=3 (field offsets 12 / 24 B: 4/8-B aligned rows) with
-    and without 16-B vectors over unaligned field addresses (knob field_unaligned16)."""
-    from ghex_amd import _ghx
-    _ghx.call("ghx_tune", b"field_unaligned16", u16)
-    try:
-        test_mixed_five_fields_config4_shape()
-        test_dtypes_exchange(np.float32)
-        test_single_domain_periodic_fp64((2, 1, 0), 1, 13)
-        test_single_domain_periodic_fp64((1, 0, 2), 3, 13)
-    finally:
-        _ghx.call("ghx_tune", b"reset", 0)
-
-
 def test_field_descriptor_pack_unpack_api_unaligned_and_components():
     """field.pack(buffer, spaces, stream) / unpack — the concept's member functions — on a
     vector field (component axis) at a misaligned base (vector-width downgrade)."""
@@ -426,8 +411,7 @@ def test_full_size_512_h2_checksum():
                                    {"short_pol": 3}, {"short_pol": 1, "small_row_bytes": 4096},
                                    {"short_pol": 2, "small_tile_rows": 64},
                                    {"tile_bytes": 65536, "small_row_bytes": 8},
-                                   {"field_unaligned16": 1},
-                                   {"field_unaligned16": 1, "short_pol": 3, "tile_bytes": 4096}],
+                                   {"short_pol": 3, "tile_bytes": 4096}],
                          ids=lambda d: "-".join(f"{k}={v}" for k, v in d.items()))
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_tuning_variants_stay_bit_exact(knobs, Hw):
