@@ -84,3 +84,15 @@ def test_stage_guard_is_silent_when_the_stage_finishes():
             "time.sleep(3); print('survived')") % ROOT
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and p.stdout.strip() == "survived"
+
+
+def test_read_floor_probe_reports_instead_of_failing_without_a_gpu():
+    """roofline.read_floor (tools/lib/libpackfloor.so) is a developer measurement: without a
+    device (or without the library) it reports an error entry, never an exception. Runs in a
+    child process (the probe's HIP runtime stays out of the test runner)."""
+    code = ("import sys, json; sys.path.insert(0, %r); import bench; "
+            "print(json.dumps(bench.pack_read_floor(8, 1, {'pack_kernel_us': 1.0})))") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-500:]
+    out = __import__("json").loads(p.stdout.strip().splitlines()[-1])
+    assert "error" in out
