@@ -124,7 +124,7 @@ struct alignas(16) seg_u
     uint8_t lid64;
     uint8_t fpol;              // field-side cache policy (as seg_s)
     uint32_t tile_bytes;
-    uint64_t reserved;
+    int64_t field_off;         // added to every field offset (a level of a split levels-last list)
     uint8_t runs;              // mode 0, rows of 4 or 8 B, rows of consecutive lids contiguous
                                // in the field: lanes move 16-B chunks (16/L rows), one 16-B
                                // field access where the chunk's lids form a run (copy_runs);

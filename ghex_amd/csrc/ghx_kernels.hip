@@ -191,7 +191,7 @@ __device__ __forceinline__ int64_t field_offset_u(const seg_u& s, uint32_t p)
         l = fastdiv(row, s.mag_inner);
         i = row - l * s.n;
     }
-    return load_lid(s, i) * s.index_stride_b + int64_t(l) * s.level_stride_b + int64_t(col);
+    return s.field_off + load_lid(s, i) * s.index_stride_b + int64_t(l) * s.level_stride_b + int64_t(col);
 }
 
 template<typename Seg>
@@ -350,7 +350,7 @@ __device__ __forceinline__ void copy_runs(const seg_u& s, char* __restrict__ fie
                 for (int j = 0; j < K; ++j) l[j] = p + j * L < end ? load_lid(s, r0 + j) : 0;
             }
 #pragma unroll
-            for (int j = 0; j < K; ++j) fo[u][j] = l[j] * L;  // index stride = L (planner)
+            for (int j = 0; j < K; ++j) fo[u][j] = s.field_off + l[j] * L;  // index stride = L (planner)
         }
         V v[kU];
 #pragma unroll

@@ -505,12 +505,18 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
     struct pending
     {
         size_t seg;
+        size_t off;  // the segment's list in the device allocation
+    };
+    struct lid_upload
+    {
         const int64_t* lids;
         int64_t n;
         bool wide;
         size_t off;
     };
     std::vector<pending> pend;
+    std::vector<lid_upload> uploads;
+    std::map<std::pair<const int64_t*, int64_t>, size_t> lid_off;
     std::vector<int32_t> gf, gb;  // caller slots per segment
     size_t lid_bytes = 0;
     for (int e = 0; e < n_entries; ++e)
@@ -524,79 +530,119 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
         max_buf_slot = std::max(max_buf_slot, en.buffer_slot);
         if (en.n_lids == 0) continue;
         const int64_t elem = d.elem_size;
-        const int64_t total = en.n_lids * d.levels * elem;
-        if (total >= (int64_t(1) << 31) - kMaxTileBytes || en.n_lids >= (int64_t(1) << 32))
-            throw invalid("unstructured segment too large");
         bool wide = false;
         for (int64_t i = 0; i < en.n_lids; ++i)
         {
             if (en.lids[i] < 0) throw invalid("negative local index");
             if (en.lids[i] >= (int64_t(1) << 31)) wide = true;
         }
-        seg_u s{};  // slots: set per launch group below
-        s.buf_off = en.buffer_offset;
-        s.n = uint32_t(en.n_lids);
-        s.index_stride_b = d.index_stride * elem;
-        s.level_stride_b = d.level_stride * elem;
-        s.lid64 = wide ? 1 : 0;
+        int mode;
         int64_t L;
         if (d.levels == 1 || (d.levels_first && d.level_stride == 1))
         {
-            s.mode = 0;  // one row per index: all levels contiguous on both sides
+            mode = 0;  // one row per index: all levels contiguous on both sides
             L = d.levels * elem;
-        }
-        else if (d.levels_first)
-        {
-            s.mode = 1;  // buf[(i*levels + l)]: rows (i, l), i-major
-            L = elem;
-            s.row_levels = uint32_t(d.levels);
-            s.mag_inner = make_magic(uint32_t(d.levels));
         }
         else
         {
-            s.mode = 2;  // buf[(l*n + i)]: rows (l, i), l-major
+            mode = d.levels_first ? 1 : 2;  // rows (i, l) i-major / rows (l, i) l-major
             L = elem;
-            s.mag_inner = make_magic(uint32_t(en.n_lids));
         }
-        s.row_bytes = uint32_t(L);
-        s.bytes = uint32_t(total);
-        s.mag_row = make_magic(uint32_t(L));
-        int w = wlog2_of(uint64_t(L));
-        w = std::min(w, wlog2_of(s.buf_off));
-        if (en.n_lids > 1) w = std::min(w, wlog2_of(uint64_t(s.index_stride_b < 0 ? -s.index_stride_b : s.index_stride_b)));
-        if (s.mode != 0) w = std::min(w, wlog2_of(uint64_t(s.level_stride_b < 0 ? -s.level_stride_b : s.level_stride_b)));
-        s.wlog2 = uint8_t(w);
-        // 4/8-B rows whose consecutive lids are adjacent in the field (index stride = row
-        // length): 16-B lane chunks, one field access per run of 16/L lids (copy_runs)
-        s.runs = (g_tune.urun && s.mode == 0 && (L == 4 || L == 8) && s.index_stride_b == L &&
-                  s.buf_off % 16 == 0) ? 1 : 0;
-        if (s.runs)
-        {
-            // run-heavy: at least half of the 16-B chunks hold 16/L consecutive lids
-            const int64_t K = 16 / L, chunks = en.n_lids / K;
-            int64_t hits = 0;
-            for (int64_t c = 0; c < chunks; ++c)
+        // one segment of index range [a, a + n) of the list (mode 2 split: one level `lev`, as
+        // a mode-0 segment of elem-byte rows at field offset lev * level stride)
+        auto add = [&](int64_t a, int64_t n, int m, int64_t lev, uint64_t buf_off) {
+            seg_u s{};  // slots: set per launch group below
+            s.buf_off = buf_off;
+            s.n = uint32_t(n);
+            s.index_stride_b = d.index_stride * elem;
+            s.level_stride_b = d.level_stride * elem;
+            s.field_off = lev >= 0 ? lev * s.level_stride_b : 0;
+            s.lid64 = wide ? 1 : 0;
+            s.mode = uint8_t(m);
+            const int64_t Ls = m == 0 && lev < 0 ? L : elem;
+            if (m == 1)
             {
-                bool run = true;
-                for (int64_t j = 1; j < K && run; ++j) run = en.lids[c * K + j] == en.lids[c * K] + j;
-                hits += run ? 1 : 0;
+                s.row_levels = uint32_t(d.levels);
+                s.mag_inner = make_magic(uint32_t(d.levels));
             }
-            if (chunks > 0 && 2 * hits >= chunks) s.runs = 2;
+            else if (m == 2)
+                s.mag_inner = make_magic(uint32_t(n));
+            const int64_t seg_bytes = n * (m == 0 ? Ls : int64_t(d.levels) * elem);
+            s.row_bytes = uint32_t(Ls);
+            s.bytes = uint32_t(seg_bytes);
+            s.mag_row = make_magic(uint32_t(Ls));
+            int w = wlog2_of(uint64_t(Ls));
+            w = std::min(w, wlog2_of(s.buf_off));
+            w = std::min(w, wlog2_of(uint64_t(s.field_off < 0 ? -s.field_off : s.field_off)));
+            if (n > 1) w = std::min(w, wlog2_of(uint64_t(s.index_stride_b < 0 ? -s.index_stride_b : s.index_stride_b)));
+            if (m != 0) w = std::min(w, wlog2_of(uint64_t(s.level_stride_b < 0 ? -s.level_stride_b : s.level_stride_b)));
+            s.wlog2 = uint8_t(w);
+            // 4/8-B rows whose consecutive lids are adjacent in the field (index stride = row
+            // length): 16-B lane chunks, one field access per run of 16/L lids (copy_runs)
+            s.runs = (g_tune.urun && m == 0 && (Ls == 4 || Ls == 8) && s.index_stride_b == Ls &&
+                      s.buf_off % 16 == 0) ? 1 : 0;
+            if (s.runs)
+            {
+                // run-heavy: at least half of the 16-B chunks hold 16/L consecutive lids
+                const int64_t K = 16 / Ls, chunks = n / K;
+                const int64_t* li = en.lids + a;
+                int64_t hits = 0;
+                for (int64_t c = 0; c < chunks; ++c)
+                {
+                    bool run = true;
+                    for (int64_t j = 1; j < K && run; ++j) run = li[c * K + j] == li[c * K] + j;
+                    hits += run ? 1 : 0;
+                }
+                if (chunks > 0 && 2 * hits >= chunks) s.runs = 2;
+            }
+            // index lists shared by the segments that read the same range (split levels)
+            const auto key = std::make_pair(en.lids + a, n);
+            auto it = lid_off.find(key);
+            size_t off;
+            if (it != lid_off.end()) off = it->second;
+            else
+            {
+                lid_bytes = (lid_bytes + 15) & ~size_t(15);
+                off = lid_bytes;
+                lid_bytes += size_t(n) * (wide ? 8 : 4);
+                lid_off.emplace(key, off);
+                uploads.push_back({en.lids + a, n, wide, off});
+            }
+            pend.push_back({segs.size(), off});
+            segs.push_back(s);
+            gf.push_back(en.field_slot);
+            gb.push_back(en.buffer_slot);
+        };
+        // a segment addresses its bytes with 32-bit offsets: lists of more than kSegLimit bytes
+        // are planned as several segments (index ranges; a levels-last list level by level)
+        constexpr int64_t kSegLimit = int64_t(1) << 30;
+        const int64_t per_index = int64_t(d.levels) * elem;
+        const int64_t total = en.n_lids * per_index;
+        if (per_index > kSegLimit) throw invalid("unstructured row of more than 1 GiB");
+        if (total <= kSegLimit && en.n_lids < (int64_t(1) << 32))
+            add(0, en.n_lids, mode, -1, en.buffer_offset);
+        else if (mode != 2)
+        {
+            const int64_t step = kSegLimit / per_index;
+            for (int64_t a = 0; a < en.n_lids; a += step)
+                add(a, std::min(step, en.n_lids - a), mode, -1,
+                    en.buffer_offset + uint64_t(a * per_index));
         }
-        lid_bytes = (lid_bytes + 15) & ~size_t(15);
-        pending pe{segs.size(), en.lids, en.n_lids, wide, lid_bytes};
-        lid_bytes += size_t(en.n_lids) * (wide ? 8 : 4);
-        pend.push_back(pe);
-        segs.push_back(s);
-        gf.push_back(en.field_slot);
-        gb.push_back(en.buffer_slot);
+        else
+        {
+            const int64_t step = kSegLimit / elem;
+            for (int64_t lev = 0; lev < d.levels; ++lev)
+                for (int64_t a = 0; a < en.n_lids; a += step)
+                    add(a, std::min(step, en.n_lids - a), 0, lev,
+                        en.buffer_offset + uint64_t((lev * en.n_lids + a) * elem));
+        }
         bytes += uint64_t(total);
     }
     n_segments = int32_t(segs.size());
     if (!segs.empty() && have_device())
     {
         std::vector<unsigned char> host(lid_bytes);
-        for (auto& p : pend)
+        for (auto& p : uploads)
         {
             if (p.wide)
             {

@@ -277,6 +277,33 @@ def test_plans_beyond_64_slots_are_cut_into_launch_groups():
     assert b"negative slot" in L.ghx_last_error()
 
 
+def test_unstructured_lists_beyond_one_segment_are_split():
+    """A segment addresses its message with 32-bit offsets: an index list of more than 1 GiB is
+    planned as several segments — index ranges, or level by level for levels-last data — and
+    the plan's byte count is unchanged (host-side planning; the device check is in
+    tests/test_gpu_large.py)."""
+    import ctypes
+    import numpy as np
+    from ghex_amd import _ghx
+    L = _ghx.lib()
+    for levels, first, n, want in ((1, 1, 1 << 21, 2), (2, 0, 1 << 20, 2), (3, 1, 1 << 19, 2),
+                                   (1, 1, 1000, 1)):
+        lids = np.arange(n, dtype=np.int64)[::-1].copy()
+        e = _ghx.UPackEntry()
+        e.data.elem_size, e.data.levels, e.data.levels_first = 1024, levels, first
+        e.data.index_stride = levels if first else 1
+        e.data.level_stride = 1 if first else n
+        e.field_slot, e.buffer_slot, e.buffer_offset = 0, 0, 0
+        e.lids = lids.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+        e.n_lids = n
+        h = ctypes.c_void_p()
+        assert L.ghx_uplan_create(ctypes.byref(e), 1, 0, ctypes.byref(h)) == 0, L.ghx_last_error()
+        nb, ns = ctypes.c_uint64(), ctypes.c_int32()
+        assert L.ghx_uplan_info(h, ctypes.byref(nb), ctypes.byref(ns), None) == 0
+        assert nb.value == n * levels * 1024 and ns.value >= want, (levels, first, ns.value)
+        assert L.ghx_uplan_destroy(h) == 0
+
+
 def test_epochs_flag_block_argument_checks_and_cleanup(ghx):
     """ghx_epochs_* (device-side access epochs of the bulk exchange) without a GPU: bad names,
     world/rank and timeouts are refused; a creating rank that cannot register the block (no
