@@ -705,6 +705,8 @@ def extras(args, torch, dist, dev, stream, out, v):
         torch.cuda.empty_cache()
         if world == 1:
             roof["read_floor"] = pack_read_floor(N, Hw, roof)
+            if "fused_self" in out:
+                out["fused_self"]["floor"] = fused_floor(N, Hw, out["fused_self"]["launch_us"])
 
     if world == 1:
         # the other BASELINE configs, per GPU (their 8-GPU forms are weak-scaled copies)
@@ -733,7 +735,29 @@ def _floor_lib():
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                       ctypes.POINTER(ctypes.c_int64)]
+    L.ghx_probe_fused_floor.restype = ctypes.c_int
+    L.ghx_probe_fused_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double)]
     return L
+
+
+def fused_floor(N, Hw, launch_us):
+    """The fused self exchange's mirror (tools/pack_floor.hip ghx_probe_fused_floor): one launch
+    that loads one vector per field line the pack reads, streams the buffer writes and writes
+    every halo piece once — k_self's memory work without its index arithmetic."""
+    import ctypes
+    try:
+        L = _floor_lib()
+        if L is None:
+            return {"error": "tools/lib/libpackfloor.so not built (make -C tools)"}
+        us = (ctypes.c_double * 2)()
+        rc = L.ghx_probe_fused_floor(N, Hw, 21, us)
+        if rc:
+            return {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
+        return {"floor_us": round(us[0], 2), "floor_cold_us": round(us[1], 2),
+                "k_self_vs_floor": round(us[0] / launch_us, 3) if launch_us else None}
+    except Exception as e:  # reported, never fatal
+        return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
 
 
 def pack_read_floor(N, Hw, roof):

@@ -88,6 +88,29 @@ __global__ __launch_bounds__(256) void k_pieces(const uint32_t* __restrict__ pie
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
 }
 
+// The fused self exchange's mirror: one grid loads one vector per pack line, streams the buffer
+// writes and writes every halo piece (what k_self must do, with no index arithmetic).
+__global__ __launch_bounds__(256) void k_fused(const uint32_t* __restrict__ lines, uint32_t nl,
+                                               const uint32_t* __restrict__ pieces, uint32_t np,
+                                               char* __restrict__ field, v4* __restrict__ buf,
+                                               uint64_t wvec, unsigned* sink)
+{
+    v4 acc{0, 0, 0, 0};
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nl; i += stride)
+        acc ^= *(const v4*)(field + uint64_t(lines[i]) * 128);
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < wvec; i += uint64_t(stride))
+        buf[i] = v4{unsigned(i), acc.x, 2, 3};
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < np; i += stride)
+    {
+        const uint32_t q = pieces[i];
+        char* a = field + uint64_t(q & 0x7fffffffu) * 8;
+        if (q >> 31) *(v4*)a = v4{q, acc.y, 2, 3};
+        else *(unsigned __attribute__((ext_vector_type(2)))*)a = {q, acc.z};
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
+}
+
 __global__ __launch_bounds__(256) void k_sweep(const v4* p, size_t n, unsigned* sink)
 {
     v4 acc{0, 0, 0, 0};
@@ -304,6 +327,67 @@ done:
     return rc;
 }
 
+// out_us[2]: {warm, cold} of the fused mirror (pack lines read + buffer written + halo pieces
+// written, one launch). Returns 0, or the failing source line.
+extern "C" int ghx_probe_fused_floor(int N, int H, int reps, double* out_us)
+{
+    int rc = 0;
+    std::vector<uint32_t> xf, lg, pxf, plg;
+    uint64_t useful = 0, useful2 = 0;
+    line_sets(N, H, xf, lg, useful);
+    piece_sets(N, H, pxf, plg, useful2);
+    std::vector<uint32_t> lines(xf), pieces(pxf);
+    lines.insert(lines.end(), lg.begin(), lg.end());
+    pieces.insert(pieces.end(), plg.begin(), plg.end());
+    const int E = N + 2 * H;
+    const size_t fbytes = size_t(E) * E * E * 8, flush_bytes = size_t(1) << 30;
+    char *field = nullptr, *fl = nullptr;
+    v4* buf = nullptr;
+    unsigned* sink = nullptr;
+    uint32_t *d_l = nullptr, *d_p = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const int grid = 256 * 8;
+    if (fbytes / 8 >= (size_t(1) << 31)) return __LINE__;
+    CK(hipMalloc(&field, fbytes));
+    CK(hipMalloc(&fl, flush_bytes));
+    CK(hipMalloc(&buf, useful + 64));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMalloc(&d_l, lines.size() * 4 + 4));
+    CK(hipMalloc(&d_p, pieces.size() * 4 + 4));
+    CK(hipMemcpy(d_l, lines.data(), lines.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_p, pieces.data(), pieces.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(field, 1, fbytes));
+    CK(hipMemset(fl, 2, flush_bytes));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int cold = 0; cold < 2; ++cold)
+    {
+        std::vector<float> t;
+        for (int i = 0; i < reps; ++i)
+        {
+            if (cold)
+                hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, 0, (const v4*)fl, flush_bytes / 16, sink);
+            else
+                hipLaunchKernelGGL(k_fused, dim3(grid), dim3(256), 0, 0, d_l, uint32_t(lines.size()), d_p,
+                                   uint32_t(pieces.size()), field, buf, useful / 16, sink);
+            hipExtLaunchKernelGGL(k_fused, dim3(grid), dim3(256), 0, 0, e0, e1, 0, d_l, uint32_t(lines.size()),
+                                  d_p, uint32_t(pieces.size()), field, buf, useful / 16, sink);
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            t.push_back(ms * 1e3f);
+        }
+        std::sort(t.begin(), t.end());
+        out_us[cold] = t[t.size() / 2];
+    }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    for (void* p : {(void*)field, (void*)fl, (void*)buf, (void*)sink, (void*)d_l, (void*)d_p})
+        if (p) (void)hipFree(p);
+    return rc;
+}
+
 #ifdef PACK_FLOOR_MAIN
 int main(int argc, char** argv)
 {
@@ -335,6 +419,14 @@ int main(int argc, char** argv)
     for (int j = 0; j < 4; ++j)
         for (int cold = 0; cold < 2; ++cold)
             printf("{\"set\": \"%s\", \"cold\": %d, \"us\": %.2f}\n", unames[j], cold, us[2 * j + cold]);
+    const int rc3 = ghx_probe_fused_floor(N, H, reps, us);
+    if (rc3)
+    {
+        printf("{\"error\": \"HIP call failed at pack_floor.hip:%d\"}\n", rc3);
+        return 1;
+    }
+    for (int cold = 0; cold < 2; ++cold)
+        printf("{\"set\": \"fused_reads_buffer_halos\", \"cold\": %d, \"us\": %.2f}\n", cold, us[cold]);
     return 0;
 }
 #endif
