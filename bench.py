@@ -64,6 +64,10 @@ def parse():
     p.add_argument("--no-layout", action="store_true",
                    help="skip the padded-layout leg (its launches share the headline kernel's "
                         "grid and would mix into a profiler's per-kernel averages)")
+    p.add_argument("--bulk-child", action="store_true",
+                   help="internal: the isolated zero-copy leg's rank process (see bulk_isolated)")
+    p.add_argument("--bulk-timeout", type=float, default=120.0,
+                   help="seconds the isolated zero-copy leg (N>1) may take before it is killed")
     p.add_argument("--bulk", action="store_true",
                    help="N>1: also time the zero-copy bulk exchange (IPC puts into peer halos); "
                         "always on at N=1 (self puts)")
@@ -218,8 +222,119 @@ class Runner:
             self.graphs[k % self.G].replay()
 
 
+def bulk_child(args):
+    """One rank of the isolated zero-copy leg (spawned by bulk_isolated, one process per rank,
+    the parent rank's GPU): the same domain and field as the headline, exchanged by
+    BulkCommunicationObject — IPC puts straight into the peers' halos over xGMI, ordered by device
+    epochs — verified (every cell = its wrapped global index) and timed. A gloo group carries the
+    setup; the data moves only through the puts. Rank 0 prints one JSON line."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(60.0, args.bulk_timeout)))
+    import ghex_amd
+    from ghex_amd.structured import regular as R
+    ghex_amd.native_library()
+    N, Hw, parts = args.N, args.halo, DECOMP[world]
+    E = N + 2 * Hw
+    G = [parts[d] * N for d in range(3)]
+    c = (rank % parts[0], (rank // parts[0]) % parts[1], rank // (parts[0] * parts[1]))
+    first = tuple(c[d] * N for d in range(3))
+    last = tuple((c[d] + 1) * N - 1 for d in range(3))
+    ctx = ghex_amd.make_context()
+    dd = R.DomainDescriptor(rank, first, last)
+    pc = R.make_pattern(ctx, R.HaloGenerator((0, 0, 0), tuple(g - 1 for g in G), (Hw,) * 6,
+                                             (True,) * 3), [dd])
+    base = torch.full((E, E, E), -1.0, dtype=torch.float64, device=dev)
+    ar = [torch.arange(N, device=dev, dtype=torch.float64) + first[d] for d in range(3)]
+    base[Hw:Hw + N, Hw:Hw + N, Hw:Hw + N] = (
+        ar[0].view(1, 1, N) + G[0] * (ar[1].view(1, N, 1) + G[1] * ar[2].view(N, 1, 1)))
+    fd = R.make_field_descriptor(dd, base.permute(2, 1, 0), (Hw,) * 3, (E,) * 3)
+    bco = ghex_amd.make_bulk_communication_object(ctx)
+    bco.add_field(pc(fd))
+    bco.init()
+    bco.exchange().wait()
+    idx = [((torch.arange(E, device=dev, dtype=torch.int64) - Hw + first[d]) % G[d]).to(torch.float64)
+           for d in range(3)]
+    expect = idx[0].view(1, 1, E) + G[0] * (idx[1].view(1, E, 1) + G[1] * idx[2].view(E, 1, 1))
+    bad = torch.tensor([float((base != expect).sum().item())])
+    del expect
+    dist.all_reduce(bad)
+
+    def timed(fn, k):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        t = torch.tensor([time.perf_counter() - t0])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+    k = min(args.steps, 50)
+    for _ in range(3):
+        bco.exchange().wait()
+    T = timed(lambda: bco.exchange(), k)
+    bco.check_epochs()
+    Tw = timed(lambda: bco.exchange().wait(), k)
+    n = E ** 3 - N ** 3
+    if rank == 0:
+        print(json.dumps({"isolated": True, "verified": bad.item() == 0,
+                          "exchange_ms_per_step": round(T / k * 1e3, 4),
+                          "exchange_wait_ms_per_step": round(Tw / k * 1e3, 4),
+                          "GBps_moved": round(world * 2 * n * 8 * k / T / 1e9, 1),
+                          "epochs": bco.epochs, "put_launches": len(bco._puts),
+                          "bytes_moved_per_step_per_gpu": 2 * n * 8,
+                          "transport": "IPC puts over xGMI (device epochs), gloo for setup only"}),
+              flush=True)
+    del bco
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def bulk_isolated(args, rank, world, local, port_of_rank0, timeout):
+    """The zero-copy exchange between GPUs, run in child processes (one per rank, spawned, not
+    exec'd) so that whatever happens there — a fault, a hang past --bulk-timeout — cannot take
+    the headline line down with it: the parent waits, kills the child's process group on expiry
+    and reports an error entry instead."""
+    import signal
+    import subprocess
+    env = dict(os.environ)
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port_of_rank0), WORLD_SIZE=str(world),
+               RANK=str(rank), LOCAL_RANK=str(local))
+    cmd = [sys.executable, os.path.abspath(__file__), "--bulk-child", "--gpus", str(world),
+           "--steps", str(args.steps), "--N", str(args.N), "--halo", str(args.halo)]
+    def die_with_parent():  # the child never outlives this rank (e.g. the extras' watchdog exit)
+        import ctypes
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)  # PR_SET_PDEATHSIG
+    cmd += ["--bulk-timeout", str(timeout)]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True, preexec_fn=die_with_parent)
+    try:
+        so, se = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        p.communicate()
+        return {"isolated": True, "error": f"timed out after {timeout:.0f} s"}
+    if p.returncode != 0:
+        return {"isolated": True, "error": f"exit {p.returncode}: {se.strip()[-300:]}"}
+    if rank != 0:
+        return None
+    lines = [l for l in so.splitlines() if l.startswith("{")]
+    return json.loads(lines[-1]) if lines else {"isolated": True, "error": "no result line"}
+
+
 def main():
     args = parse()
+    if args.bulk_child:
+        return bulk_child(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_workers(args))  # before anything touches the GPU
     import threading
@@ -528,6 +643,8 @@ def extras(args, torch, dist, dev, stream, out, v):
     n_halo, step_bytes, launch_bytes = v["n_halo"], v["step_bytes"], v["launch_bytes"]
     ghex_amd, R, L, _ghx, N, Hw = v["ghex_amd"], v["R"], v["L"], v["_ghx"], v["N"], v["Hw"]
     roof = out["roofline"]
+    all_reduce_host, local = v["all_reduce_host"], v["local"]
+    t_extras = time.perf_counter()
 
     if not args.no_cold:
         # Cold caches: an application's stencil sweeps the whole field between exchanges, so the
@@ -647,6 +764,30 @@ def extras(args, torch, dist, dev, stream, out, v):
         # the same cells and bytes in a field whose x rows are allocated 2 cells wider (row pitch
         # 4,144 B instead of 4,128 B): what the x-face lines' address set costs
         out["layout_x_alloc_518"] = bench_halo(Hw, v, torch, dist, dev, stream, args, x_alloc=518)
+    if world > 1 and not args.bulk:
+        # the zero-copy exchange between GPUs, isolated in child processes (bulk_isolated); every
+        # rank takes part (the children rendezvous among themselves on a fresh port)
+        try:
+            import socket
+            port = 0
+            if rank == 0:
+                sk = socket.socket()
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+                sk.close()
+            port = int(all_reduce_host(float(port), dist.ReduceOp.MAX))
+            # inside the extras' own budget (the watchdog prints without them at
+            # --extras-timeout): every rank agrees on the time the children get
+            left = args.extras_timeout - (time.perf_counter() - t_extras) - 30.0
+            left = all_reduce_host(left, dist.ReduceOp.MIN)
+            if left < 30.0:
+                res = {"isolated": True, "error": "skipped: the extras' time budget is spent"}
+            else:
+                res = bulk_isolated(args, rank, world, local, port, min(args.bulk_timeout, left))
+            if rank == 0:
+                out["bulk"] = res
+        except Exception as e:  # reported, never fatal for the headline measurement
+            out["bulk"] = {"isolated": True, "error": f"{type(e).__name__}: {str(e)[:200]}"}
     if world == 1 or args.bulk:
         # zero-copy bulk exchange (BulkCommunicationObject): puts straight into the
         # receivers' halos, no buffers: 2*n*8 bytes moved per step (not the metric's 4*n*8)

@@ -96,3 +96,15 @@ def test_read_floor_probe_reports_instead_of_failing_without_a_gpu():
     assert p.returncode == 0, p.stderr[-500:]
     out = __import__("json").loads(p.stdout.strip().splitlines()[-1])
     assert "error" in out
+
+
+def test_isolated_bulk_leg_reports_a_failed_child():
+    """bench.py's zero-copy leg at N>1 runs in child processes: a child that fails (here: no GPU)
+    becomes an error entry in the line; the rank itself carries on."""
+    code = ("import sys, json, types; sys.path.insert(0, %r); import bench\n"
+            "a = types.SimpleNamespace(steps=5, N=8, halo=1, bulk_timeout=60.0)\n"
+            "print(json.dumps(bench.bulk_isolated(a, 0, 2, 0, 29517, 60.0)))") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-500:]
+    out = __import__("json").loads(p.stdout.strip().splitlines()[-1])
+    assert out["isolated"] and "error" in out
