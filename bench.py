@@ -289,7 +289,8 @@ def bulk_child(args):
                           "GBps_moved": round(world * 2 * n * 8 * k / T / 1e9, 1),
                           "epochs": bco.epochs, "put_launches": len(bco._puts),
                           "bytes_moved_per_step_per_gpu": 2 * n * 8,
-                          "transport": "IPC puts over xGMI (device epochs), gloo for setup only"}),
+                          "transport": "IPC puts into the peers' fields (over xGMI between GPUs), "
+                                       "device epochs; gloo for setup only"}),
               flush=True)
     del bco
     dist.barrier()
