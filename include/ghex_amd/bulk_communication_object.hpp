@@ -14,8 +14,10 @@
 // receiver's recv halo of one key describe the same virtual message bytes; one launch per group
 // of up to 64 messages) on the object's stream. Peer fields are mapped once in init(): through
 // IPC handles (ghx_ipc_export/import) for ranks in other processes of this host, directly for
-// ranks that are threads of this process (loopback transport). Ranks on other hosts: throws
-// (their exchanges use communication_object).
+// ranks that are threads of this process (loopback transport). Halos from and to ranks on other
+// hosts go through a communication_object over the pattern's remote part (ghx_pattern_filter),
+// started by the same exchange() and awaited by the same wait() — the reference's split into
+// local (RMA) and remote pattern maps (bulk_communication_object.hpp:330-383).
 //
 // Epochs (the reference's access guards, include/ghex/rma/access_guard.hpp:35-140, and its
 // open / put-when-writable / wait sequence, bulk_communication_object.hpp:621-694). Ranks in
@@ -38,6 +40,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -50,6 +53,7 @@ class bulk_handle
 {
     hipEvent_t m_done = nullptr;       // the object's completion event (device epochs)
     const ghx_epochs* m_ep = nullptr;
+    communication_handle m_remote;     // the halos exchanged with other hosts' ranks
 
     void check() const
     {
@@ -64,21 +68,23 @@ class bulk_handle
 
   public:
     bulk_handle() = default;
-    bulk_handle(hipEvent_t done, const ghx_epochs* ep)
+    bulk_handle(hipEvent_t done, const ghx_epochs* ep, communication_handle remote = {})
     : m_done{done}
     , m_ep{ep}
+    , m_remote{remote}
     {
     }
     void wait()
     {
         if (m_done) check_hip(hipEventSynchronize(m_done), "hipEventSynchronize");
         check();
+        m_remote.wait();
     }
     bool is_ready()
     {
         if (m_done && hipEventQuery(m_done) != hipSuccess) return false;
         check();
-        return true;
+        return m_remote.is_ready();
     }
     void progress() { (void)is_ready(); }
 };
@@ -93,6 +99,7 @@ class bulk_communication_object
         void* data;
         int domain;
         int j;  // the j-th field registered for this domain on this rank
+        int align;  // alignof(value_type): the buffer layout of the remote part
     };
     struct remote_space_key
     {
@@ -126,12 +133,18 @@ class bulk_communication_object
     std::vector<put> m_puts;
     std::vector<void*> m_imports;
     bool m_init = false;
-    ghx_epochs* m_ep = nullptr;        // device epochs (all peers in other processes)
-    std::string m_ep_name;             // rank 0: the flag block it created for this object
+    ghx_epochs* m_ep = nullptr;        // device epochs (this host's ranks all separate processes)
     hipEvent_t m_after = nullptr, m_done = nullptr;
+    std::string m_host;                // set_host_name(): tests emulate several hosts
+    // the remote part: halos exchanged with ranks on other hosts, buffered
+    std::vector<std::unique_ptr<pattern_container>> m_rpcs;
+    std::vector<ghx_exchange_item> m_ritems;
+    std::vector<void*> m_rptrs;
+    std::unique_ptr<communication_object> m_remote;
 
-    static std::string hostname()
+    std::string hostname() const
     {
+        if (!m_host.empty()) return m_host;
         char buf[256] = {0};
         if (gethostname(buf, sizeof(buf) - 1) != 0) return "?";
         return buf;
@@ -166,8 +179,7 @@ class bulk_communication_object
         detail::put(out, std::int32_t(host.size()));
         out.insert(out.end(), host.begin(), host.end());
         detail::put(out, std::int64_t(getpid()));
-        detail::put(out, std::int32_t(m_ep_name.size()));
-        out.insert(out.end(), m_ep_name.begin(), m_ep_name.end());
+        detail::put(out, std::int32_t(0));  // (the epochs name travels in init()'s second round)
         detail::put(out, std::int32_t(m_fields.size()));
         for (const auto& f : m_fields)
         {
@@ -308,7 +320,8 @@ class bulk_communication_object
                       "bulk (zero-copy) exchange is implemented for structured fields");
         if (m_init) throw std::runtime_error("this bulk communication object has been initialized already");
         local_field f{bi.pattern, bi.local_index, bi.field->desc(),
-                      const_cast<void*>(static_cast<const void*>(bi.field->data())), int(bi.field->domain_id()), 0};
+                      const_cast<void*>(static_cast<const void*>(bi.field->data())), int(bi.field->domain_id()), 0,
+                      int(alignof(typename Field::value_type))};
         for (const auto& g : m_fields) f.j += g.domain == f.domain;
         m_fields.push_back(f);
     }
@@ -319,38 +332,50 @@ class bulk_communication_object
         if (m_init) return;
         const int me = m_ctx->rank();
         const int world = m_ctx->size();
-        if (me == 0 && world > 1)
-        {
-            // created before the all-gather so the others can attach after it (if they all live
-            // in other processes; otherwise it is dropped again below)
-            m_ep_name = "/ghx_ep_" + std::to_string(getpid()) + "_" +
-                        std::to_string(reinterpret_cast<std::uintptr_t>(this) & 0xffffffu);
-            check_ghx(ghx_epochs_create(m_ep_name.c_str(), 1, world, 0, epoch_timeout, &m_ep),
-                      "ghx_epochs_create");
-        }
         const auto gathered = m_ctx->get_transport().all_gather(serialize_mine());
         std::vector<remote_rank> all;
         for (const auto& g : gathered) all.push_back(deserialize(g));
         const auto& mine = all[std::size_t(me)];
-        for (std::size_t r = 0; r < all.size(); ++r)
-            if (all[r].host != mine.host)
-                throw std::runtime_error("rank " + std::to_string(r) + " is on another host (" + all[r].host +
-                                         "): zero-copy puts need node-local peers; use communication_object");
-        bool distinct = world > 1;  // every rank its own process: device epochs
-        for (std::size_t r = 0; r < all.size() && distinct; ++r)
-            for (std::size_t q = 0; q < r && distinct; ++q) distinct = all[r].pid != all[q].pid;
-        if (distinct && me != 0)
-            check_ghx(ghx_epochs_create(all[0].epochs.c_str(), 0, world, me, epoch_timeout, &m_ep),
-                      "ghx_epochs_create");
-        if (world > 1) barrier();  // every rank attached (or decided not to)
-        if (me == 0 && world > 1)
+        // this host's ranks get puts; the others' halos go through the remote part
+        std::vector<char> local(std::size_t(world), 0);
+        std::vector<std::int32_t> remote_ranks;
+        int leader = -1, nlocal = 0;
+        bool distinct = true;  // every rank of this host its own process: device epochs
+        for (int r = 0; r < world; ++r)
         {
-            (void)ghx_epochs_unlink(m_ep_name.c_str());
-            if (!distinct)
+            local[std::size_t(r)] = all[std::size_t(r)].host == mine.host;
+            if (!local[std::size_t(r)])
             {
-                ghx_epochs_destroy(m_ep);
-                m_ep = nullptr;
+                remote_ranks.push_back(r);
+                continue;
             }
+            if (leader < 0) leader = r;
+            ++nlocal;
+            for (int q = 0; q < r; ++q)
+                if (local[std::size_t(q)] && all[std::size_t(q)].pid == all[std::size_t(r)].pid) distinct = false;
+        }
+        distinct = distinct && nlocal > 1;
+        // one flag block per host: its lowest rank creates it, publishes the name in a second
+        // round, the others attach, the creator unlinks it once all have
+        std::string name;
+        if (distinct && me == leader)
+        {
+            name = "/ghx_ep_" + std::to_string(getpid()) + "_" +
+                   std::to_string(reinterpret_cast<std::uintptr_t>(this) & 0xffffffu);
+            check_ghx(ghx_epochs_create(name.c_str(), 1, world, me, epoch_timeout, &m_ep), "ghx_epochs_create");
+        }
+        if (world > 1)
+        {
+            const auto names = m_ctx->get_transport().all_gather(std::vector<char>(name.begin(), name.end()));
+            if (distinct && me != leader)
+            {
+                const auto& ln = names[std::size_t(leader)];
+                check_ghx(ghx_epochs_create(std::string(ln.begin(), ln.end()).c_str(), 0, world, me, epoch_timeout,
+                                            &m_ep),
+                          "ghx_epochs_create");
+            }
+            barrier();  // every rank attached
+            if (distinct && me == leader) (void)ghx_epochs_unlink(name.c_str());
         }
         if (m_ep)
         {
@@ -361,7 +386,8 @@ class bulk_communication_object
                     {
                         const int rr = std::get<1>(h);
                         auto& v = dir == 0 ? tgts : srcs;
-                        if (rr != me && std::find(v.begin(), v.end(), rr) == v.end()) v.push_back(rr);
+                        if (rr != me && local[std::size_t(rr)] && std::find(v.begin(), v.end(), rr) == v.end())
+                            v.push_back(rr);
                     }
             std::sort(srcs.begin(), srcs.end());
             std::sort(tgts.begin(), tgts.end());
@@ -370,6 +396,34 @@ class bulk_communication_object
                       "ghx_epochs_peers");
             check_hip(hipEventCreateWithFlags(&m_after, hipEventDisableTiming), "hipEventCreate");
             check_hip(hipEventCreateWithFlags(&m_done, hipEventDisableTiming), "hipEventCreate");
+        }
+        if (!remote_ranks.empty())
+        {
+            // the remote part: each pattern container filtered to the other hosts' ranks, every
+            // field registered with it, exchanged by a communication_object
+            std::map<const pattern_container*, std::size_t> filtered;
+            for (const auto& f : m_fields)
+            {
+                if (!filtered.count(f.pattern))
+                {
+                    ghx_pattern* out = nullptr;
+                    check_ghx(ghx_pattern_filter(f.pattern->handle(), remote_ranks.data(),
+                                                 std::int32_t(remote_ranks.size()), 1, &out),
+                              "ghx_pattern_filter");
+                    m_rpcs.push_back(std::make_unique<pattern_container>(out));
+                    filtered[f.pattern] = m_rpcs.size() - 1;
+                }
+                ghx_exchange_item it;
+                std::memset(&it, 0, sizeof(it));
+                it.pattern = m_rpcs[filtered[f.pattern]]->handle();
+                it.local_index = f.local_index;
+                it.kind = 0;
+                it.field = f.desc;
+                it.align = f.align;
+                m_ritems.push_back(it);
+                m_rptrs.push_back(f.data);
+            }
+            m_remote = std::make_unique<communication_object>(*m_ctx);
         }
         std::map<std::tuple<int, int, int>, std::pair<int, int>> target;  // (rank, domain, j)
         for (std::size_t r = 0; r < all.size(); ++r)
@@ -381,6 +435,7 @@ class bulk_communication_object
             const auto& f = m_fields[k];
             for (auto& [rid, rr, tag, boxes] : halos(*f.pattern, f.local_index, 0))
             {
+                if (!local[std::size_t(rr)]) continue;  // the remote part's
                 const auto t = target.find({rr, rid, f.j});
                 if (t == target.end())
                     throw std::runtime_error("rank " + std::to_string(rr) + " registered no field #" +
@@ -446,6 +501,7 @@ class bulk_communication_object
     bulk_handle exchange(hipStream_t after = nullptr)
     {
         if (!m_init) init();
+        communication_handle rh;
         if (m_ep)
         {
             // stream-ordered: the object's stream follows `after` (or the device), the epochs
@@ -456,6 +512,7 @@ class bulk_communication_object
                 check_hip(hipStreamWaitEvent(m_stream, m_after, 0), "hipStreamWaitEvent");
             }
             else check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            if (m_remote) rh = m_remote->start(after, m_ritems, m_rptrs);  // other hosts' halos
             check_ghx(ghx_epochs_enqueue(m_ep, 0, m_stream), "ghx_epochs_enqueue(open)");
             for (auto& p : m_puts)
                 check_ghx(ghx_put_execute(p.h, p.src.data(), std::int32_t(p.src.size()), p.dst.data(),
@@ -463,11 +520,16 @@ class bulk_communication_object
                           "ghx_put_execute");
             check_ghx(ghx_epochs_enqueue(m_ep, 1, m_stream), "ghx_epochs_enqueue(close)");
             check_hip(hipEventRecord(m_done, m_stream), "hipEventRecord");
-            if (after) check_hip(hipStreamWaitEvent(after, m_done, 0), "hipStreamWaitEvent");
-            return {m_done, m_ep};
+            if (after)
+            {
+                check_hip(hipStreamWaitEvent(after, m_done, 0), "hipStreamWaitEvent");
+                rh.schedule_wait(after);
+            }
+            return {m_done, m_ep, rh};
         }
         if (after) check_hip(hipStreamSynchronize(after), "hipStreamSynchronize");
         else check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        if (m_remote) rh = m_remote->start(nullptr, m_ritems, m_rptrs);
         barrier();  // every target open
         for (auto& p : m_puts)
             check_ghx(ghx_put_execute(p.h, p.src.data(), std::int32_t(p.src.size()), p.dst.data(),
@@ -475,8 +537,17 @@ class bulk_communication_object
                       "ghx_put_execute");
         check_hip(hipStreamSynchronize(m_stream), "hipStreamSynchronize");
         barrier();  // every halo of every rank written
-        return {};
+        if (after) rh.schedule_wait(after);
+        return {nullptr, nullptr, rh};
     }
+
+    // tests: the host name this rank reports (several hosts emulated in one process)
+    void set_host_name(std::string host)
+    {
+        if (m_init) throw std::runtime_error("set_host_name before init()");
+        m_host = std::move(host);
+    }
+    bool has_remote_part() const { return m_remote != nullptr; }
 
     // bytes moved per exchange by this rank's puts
     std::uint64_t bytes_per_exchange() const

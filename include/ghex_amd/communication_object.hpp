@@ -433,6 +433,7 @@ class communication_object
 
   private:
     friend class communication_handle;
+    friend class bulk_communication_object;  // starts the remote part of a bulk exchange
     void finish()
     {
         check_hip(hipEventSynchronize(m_done), "hipEventSynchronize");

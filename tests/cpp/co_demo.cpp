@@ -11,6 +11,9 @@
 //   co_demo bulkloop PX PY PZ N H       the same two fields through the C++
 //                                        bulk_communication_object (zero-copy puts between the
 //                                        thread-ranks' fields, no buffers)
+//   co_demo bulkhosts PX PY PZ N H K    bulkloop with the ranks spread over K emulated hosts
+//                                        (rank r on host r % K): puts between ranks of one host,
+//                                        the other halos through the bulk object's remote part
 //   co_demo rma NRANKS                  test_local_rma.cpp's geometry (two domains per rank,
 //                                        offset 3 > halo 2, double/float/int fields) through the
 //                                        C++ bulk_communication_object
@@ -65,7 +68,8 @@ struct cube
 
 // one rank: its domain, two fields, exchange twice, count bad cells
 long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, int H,
-                         communication_object::options opt, int reps = 2, bool bulk = false)
+                         communication_object::options opt, int reps = 2, bool bulk = false,
+                         int hosts = 0)
 {
     check_hip(hipSetDevice(0), "hipSetDevice");
     context ctx(t);
@@ -98,6 +102,7 @@ long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, i
     bulk_communication_object bco(ctx);
     if (bulk)
     {
+        if (hosts > 0) bco.set_host_name("host" + std::to_string(r % hosts));  // emulated hosts
         bco.add_field(pattern(fd));
         bco.add_field(pattern(ff));
         bco.init();
@@ -124,14 +129,16 @@ long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, i
                     bad += of[std::size_t(cb.idx(x, y, z))] != float(e + 1.0);
                 }
     }
-    std::printf("{\"mode\":\"%s\",\"rank\":%d,\"plans\":%zu,\"puts\":%zu,\"bad\":%ld}\n",
-                bulk ? "bulk" : "structured", r, co.num_plans(), bco.num_puts(), bad);
+    std::printf("{\"mode\":\"%s\",\"rank\":%d,\"plans\":%zu,\"puts\":%zu,\"remote\":%d,\"bad\":%ld}\n",
+                bulk ? "bulk" : "structured", r, co.num_plans(), bco.num_puts(), bco.has_remote_part() ? 1 : 0,
+                bad);
     (void)hipFree(dd);
     (void)hipFree(df);
     return bad;
 }
 
-int loopback(int px, int py, int pz, int N, int H, bool pipelined = false, bool bulk = false)
+int loopback(int px, int py, int pz, int N, int H, bool pipelined = false, bool bulk = false,
+             int hosts = 0)
 {
     const int n = px * py * pz;
     loopback_hub hub(n);
@@ -146,7 +153,7 @@ int loopback(int px, int py, int pz, int N, int H, bool pipelined = false, bool 
             {
                 communication_object::options opt;
                 opt.pipelined = pipelined;
-                bad += run_structured_rank(ts[std::size_t(r)], {px, py, pz}, N, H, opt, 2, bulk);
+                bad += run_structured_rank(ts[std::size_t(r)], {px, py, pz}, N, H, opt, 2, bulk, hosts);
             }
             catch (const std::exception& e)
             {
@@ -429,6 +436,9 @@ int main(int argc, char** argv)
         if (mode == "bulkloop" && argc == 7)
             return loopback(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
                             std::atoi(argv[6]), false, true);
+        if (mode == "bulkhosts" && argc == 8)
+            return loopback(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                            std::atoi(argv[6]), false, true, std::atoi(argv[7]));
         if (mode == "rma" && argc == 3) return rma_case(std::atoi(argv[2]));
         if (mode == "rccl" && argc == 5) return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
         if (mode == "rccl" && argc == 6)

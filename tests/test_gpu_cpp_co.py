@@ -154,6 +154,19 @@ def test_co_bulk_loopback(parts, N, H):
     assert all(l["bad"] == 0 and l["puts"] >= 1 and l["plans"] == 0 for l in ranks)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,hosts", [((2, 2, 1), 2), ((2, 2, 2), 2), ((2, 2, 2), 4)])
+def test_co_bulk_emulated_hosts(parts, hosts):
+    """The C++ bulk object with its ranks spread over emulated hosts: node-local halos by puts,
+    the others through the remote part (the pattern filtered to other hosts' ranks, a
+    communication_object over the loopback transport), one exchange()/wait(); every cell."""
+    rc, lines, err = _run(["bulkhosts", *parts, 6, 2, hosts])
+    ranks = [l for l in lines if l.get("mode") == "bulk"]
+    assert rc == 0, (lines, err)
+    assert len(ranks) == parts[0] * parts[1] * parts[2]
+    assert all(l["bad"] == 0 and l["remote"] == 1 for l in ranks)
+
+
 def test_bulk_header_compiles_host_only(tmp_path):
     """The bulk header is plain host C++ too."""
     src = tmp_path / "b.cpp"
