@@ -304,7 +304,9 @@ def bulk_isolated(args, rank, world, local, port_of_rank0, timeout):
     and reports an error entry instead."""
     import signal
     import subprocess
-    env = dict(os.environ)
+    # under torchrun the rank's env says "use the agent's store" (TORCHELASTIC_USE_AGENT_STORE):
+    # the children rendezvous on their own port instead, rank 0's child hosting the store
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port_of_rank0), WORLD_SIZE=str(world),
                RANK=str(rank), LOCAL_RANK=str(local))
     cmd = [sys.executable, os.path.abspath(__file__), "--bulk-child", "--gpus", str(world),
