@@ -465,6 +465,7 @@ void build_mixed(exchange_plan& ex, int32_t me, const std::vector<ghx_pack_entry
     // (tools/emu_rank_bench.py, profiles/r01c_emu_rank.jsonl).
     if (!short_self && !g_tune.mixed_always) return;
     upload_segments(ex.mixed_comp, comp);
+    ex.mixed_max_field_slot = su.max_field_slot;
     ex.punpack = std::make_unique<splan>(peer_e.data(), int(peer_e.size()), 1);
     ex.mixed = true;
 }
@@ -1142,7 +1143,10 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
             throw invalid("exchange is not an all-self exchange with matching segments");
         const splan& p = ex->self_pack ? *ex->self_pack : *ex->spack;
         const splan& q = ex->self_unpack ? *ex->self_unpack : *ex->sunpack;
-        if (n_fields <= p.max_field_slot || n_buffers <= p.max_buf_slot)
+        // the launch reads the pack segments' field slots AND the unpack segments' (a domain
+        // that only receives has a field slot no pack segment names, possibly the highest)
+        const int nfs = std::max(p.max_field_slot, q.max_field_slot);
+        if (n_fields <= nfs || n_buffers <= p.max_buf_slot)
             throw invalid("pointer arrays do not cover the plan's slots");
         if (!p.dev.segs || !q.dev.segs) throw hip_error("plan has no device tables");
         kargs a{};
@@ -1150,7 +1154,7 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
         a.segs2 = q.dev.segs;
         a.tile_seg = p.dev.tiles;
         a.n_tiles = p.n_tiles;
-        for (int i = 0; i <= p.max_field_slot; ++i)
+        for (int i = 0; i <= nfs; ++i)
         {
             if (!field_ptrs[i]) throw invalid("null field pointer");
             a.field_ptr[i] = reinterpret_cast<uint64_t>(field_ptrs[i]);
@@ -1182,7 +1186,9 @@ int ghx_exchange_pack_self(const ghx_exchange* ex, void* const* field_ptrs, int3
         if (!ex->mixed) throw invalid("exchange has no mixed self/peer plan (ghx_exchange_mixed)");
         const splan& p = *ex->spack;
         if (n_send < int32_t(ex->send.size())) throw invalid("too few send buffers");
-        if (n_fields <= p.max_field_slot || n_send <= p.max_buf_slot)
+        // the self messages' unpack (companion) segments name receiving fields too
+        const int nfs = std::max(p.max_field_slot, ex->mixed_max_field_slot);
+        if (n_fields <= nfs || n_send <= p.max_buf_slot)
             throw invalid("pointer arrays do not cover the plan's slots");
         if (!p.dev.segs || !ex->mixed_comp.segs) throw hip_error("plan has no device tables");
         kargs a{};
@@ -1190,7 +1196,7 @@ int ghx_exchange_pack_self(const ghx_exchange* ex, void* const* field_ptrs, int3
         a.segs2 = ex->mixed_comp.segs;
         a.tile_seg = p.dev.tiles;
         a.n_tiles = p.n_tiles;
-        for (int i = 0; i <= p.max_field_slot; ++i)
+        for (int i = 0; i <= nfs; ++i)
         {
             if (!field_ptrs[i]) throw invalid("null field pointer");
             a.field_ptr[i] = reinterpret_cast<uint64_t>(field_ptrs[i]);

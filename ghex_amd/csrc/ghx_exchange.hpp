@@ -28,6 +28,7 @@ struct exchange_plan
     // segment of its self message (zero = a peer message: pack only), and the unpack plan of
     // the peer messages alone
     device_tables mixed_comp;
+    int mixed_max_field_slot = -1;  // the highest field slot mixed_comp's segments name
     std::unique_ptr<splan> punpack;
     bool mixed = false;
     int32_t n_items = 0;

@@ -154,6 +154,17 @@ def test_more_slots_than_one_launch_holds():
               "periodic": (1, 1, 1), "fields": fields, "mixed": False, "seed": 64})
 
 
+def test_receive_only_field_slot_in_mixed_exchange():
+    """Seed 249 (found by the soak, tools/fuzz_soak.py): 2 ranks x 12-15 thin domains, a y- halo
+    only and no y periodicity, so the highest field slot of a rank belongs to a domain that only
+    receives. The mixed launch (ghx_exchange_pack_self) writes that domain's self-message halos
+    from the pack registers; it must fill the field slots its companion unpack segments name,
+    not only the pack segments' (round-3 regression: a null field pointer in the kernel)."""
+    from tests.gpu_util import emulated_exchange
+    run_case(draw_case(249))
+    assert emulated_exchange.mixed_ranks >= 1
+
+
 # ---------------------------------------------------------------------------------------------
 # unstructured: random meshes, the reference tests' halo property
 # ---------------------------------------------------------------------------------------------

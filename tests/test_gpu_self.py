@@ -119,3 +119,48 @@ def test_self_kernel_variants_stay_bit_exact(knobs, Hw):
         test_fused_equals_unfused_and_oracle(Hw, (0, 2, 1))
     finally:
         _ghx.call("ghx_tune", b"reset", 0)
+
+
+@pytest.mark.parametrize("order", ["sender_first", "receiver_first"])
+@pytest.mark.parametrize("fused", [True, False])
+def test_receive_only_domain_field_slot(order, fused):
+    """Two domains of ONE rank stacked in y, non-periodic, a y- halo only: the lower domain only
+    sends, the upper only receives, so one field slot is named by unpack segments alone. Put
+    last in the exchange() arguments it is the highest slot, which the fused launch must fill
+    from the unpack plan (round-3 regression: it filled up to the pack plan's highest slot and
+    the kernel wrote through a null field pointer). Every cell against the expected halo."""
+    import torch
+    from ghex_amd.structured import regular as R
+    from tests.gpu_util import FakeContext
+    gf, gl, halos = (0, 0, 0), (3, 7, 3), (0, 0, 2, 0, 0, 0)
+    doms = {"lo": (10, (0, 0, 0), (3, 3, 3)), "hi": (11, (0, 4, 0), (3, 7, 3))}
+    names = ["lo", "hi"] if order == "sender_first" else ["hi", "lo"]
+    ctx = FakeContext(0, 1, {0: [doms[n] for n in names]})
+    dds = [R.DomainDescriptor(*doms[n]) for n in names]
+    pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, halos, (False,) * 3), dds)
+    fields, expect, bis = [], [], []
+    for n, dd in zip(names, dds):
+        _, first, _ = doms[n]
+        a = np.full((4, 6, 4), -1.0)  # memory order (z, y, x); y: 2 halo rows + 4 owned
+        z, y, x = np.meshgrid(np.arange(4), np.arange(4), np.arange(4), indexing="ij")
+        a[:, 2:, :] = x + 4 * (y + first[1] + 8 * z)
+        e = a.copy()
+        if n == "hi":  # halo rows = global y 2, 3 of the lower domain
+            zz, yy, xx = np.meshgrid(np.arange(4), np.arange(2), np.arange(4), indexing="ij")
+            e[:, :2, :] = xx + 4 * (yy + 2 + 8 * zz)
+        base = torch.from_numpy(a).cuda()
+        fd = R.make_field_descriptor(dd, base.permute(2, 1, 0), (0, 2, 0), (4, 6, 4))
+        bis.append(pc(fd))
+        fields.append(base)
+        expect.append(e)
+    co = R.make_communication_object(ctx)
+    plan = co.plan(bis)
+    assert co.all_self(plan)
+    if fused:
+        co.exchange(bis).wait()
+    else:
+        co.pack_only(bis)
+        co.unpack_only(bis)
+    torch.cuda.synchronize()
+    for base, e in zip(fields, expect):
+        np.testing.assert_array_equal(base.cpu().numpy(), e)
