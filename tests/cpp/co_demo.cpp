@@ -27,12 +27,23 @@
 //                                        every halo value vs its owner's encoding
 //   co_demo bench N H ITERS              one rank, host-inclusive microseconds per exchange
 //                                        (exchange + wait) on the fused self path
+//   co_demo shm NAME RANK PX PY PZ N H MODE [HOSTS]
+//                                        ONE rank of a PX*PY*PZ job, this process (start one
+//                                        process per rank; shm_transport NAME): MODE plain (one
+//                                        group), pipe (per-peer lanes) or bulk (zero-copy puts
+//                                        over IPC with device epochs between the processes;
+//                                        HOSTS > 0 spreads the ranks over emulated hosts, the
+//                                        other hosts' halos through the bulk object's remote part)
+//   co_demo shmgather NAME RANK WORLD ROUNDS
+//                                        the shm transport's all_gather alone (no GPU calls):
+//                                        contributions of varying size, every byte checked
 // Prints one JSON line per rank / result; exit status 0 iff every cell matched.
 #include <ghex_amd/bulk_communication_object.hpp>
 #include <ghex_amd/communication_object.hpp>
 #include <ghex_amd/data_descriptor.hpp>
 #include <ghex_amd/field_descriptor.hpp>
 #include <ghex_amd/rccl_transport.hpp>
+#include <ghex_amd/shm_transport.hpp>
 
 #include <atomic>
 #include <chrono>
@@ -129,9 +140,10 @@ long run_structured_rank(transport& t, const std::array<int, 3>& parts, int N, i
                     bad += of[std::size_t(cb.idx(x, y, z))] != float(e + 1.0);
                 }
     }
-    std::printf("{\"mode\":\"%s\",\"rank\":%d,\"plans\":%zu,\"puts\":%zu,\"remote\":%d,\"bad\":%ld}\n",
+    std::printf("{\"mode\":\"%s\",\"rank\":%d,\"plans\":%zu,\"puts\":%zu,\"remote\":%d,\"epochs\":%d,"
+                "\"bad\":%ld}\n",
                 bulk ? "bulk" : "structured", r, co.num_plans(), bco.num_puts(), bco.has_remote_part() ? 1 : 0,
-                bad);
+                bco.device_epochs() ? 1 : 0, bad);
     (void)hipFree(dd);
     (void)hipFree(df);
     return bad;
@@ -394,6 +406,40 @@ int rma_case(int n)
     return (bad == 0 && errors == 0) ? 0 : 1;
 }
 
+// one rank per process over the shm transport (see the header)
+int shm_rank(const char* name, int rank, int px, int py, int pz, int N, int H, const std::string& mode,
+             int hosts)
+{
+    if (mode != "plain" && mode != "pipe" && mode != "bulk") throw std::runtime_error("MODE: plain|pipe|bulk");
+    const int n = px * py * pz;
+    // channels sized for the largest message group of the test geometries (two fields)
+    const std::size_t face = std::size_t(N + 2 * H) * std::size_t(N + 2 * H) * std::size_t(H) * 12;
+    shm_transport t(name, rank, n, std::size_t(1) << 20, 8 + 26 * (16 + 8) + 26 * face);
+    communication_object::options opt;
+    opt.pipelined = mode == "pipe";
+    return run_structured_rank(t, {px, py, pz}, N, H, opt, 2, mode == "bulk", hosts) == 0 ? 0 : 1;
+}
+
+int shm_gather(const char* name, int rank, int world, int rounds)
+{
+    shm_transport t(name, rank, world, std::size_t(1) << 16, 4096);
+    long bad = 0;
+    for (int round = 0; round < rounds; ++round)
+    {
+        std::vector<char> mine(std::size_t((rank * 131 + round * 17) % 4000), char(rank * 7 + round));
+        const auto all = t.all_gather(mine);
+        bad += all.size() != std::size_t(world);
+        for (int q = 0; q < world && q < int(all.size()); ++q)
+        {
+            bad += all[std::size_t(q)].size() != std::size_t((q * 131 + round * 17) % 4000);
+            for (char c : all[std::size_t(q)]) bad += c != char(q * 7 + round);
+        }
+        if (round % 7 == 3) t.barrier();
+    }
+    std::printf("{\"mode\":\"shmgather\",\"rank\":%d,\"rounds\":%d,\"bad\":%ld}\n", rank, rounds, bad);
+    return bad == 0 ? 0 : 1;
+}
+
 int bench(int N, int H, int iters)
 {
     check_hip(hipSetDevice(0), "hipSetDevice");
@@ -445,6 +491,11 @@ int main(int argc, char** argv)
             return rccl(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]));
         if (mode == "unstructured" && argc == 4) return unstructured_case(argv[2], std::atoi(argv[3]));
         if (mode == "bench" && argc == 5) return bench(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
+        if (mode == "shm" && (argc == 10 || argc == 11))
+            return shm_rank(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]),
+                            std::atoi(argv[7]), std::atoi(argv[8]), argv[9], argc == 11 ? std::atoi(argv[10]) : 0);
+        if (mode == "shmgather" && argc == 6)
+            return shm_gather(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]));
     }
     catch (const std::exception& e)
     {

@@ -192,3 +192,74 @@ def test_co_bulk_reference_local_rma_geometry(n):
     ranks = [l for l in lines if l.get("mode") == "rma"]
     assert rc == 0, (lines, err)
     assert len(ranks) == n and all(l["bad"] == 0 and l["puts"] >= 1 for l in ranks)
+
+
+def _run_procs(args_of_rank, n, timeout=120):
+    """One co_demo process per rank (shm transport); every process's lines and exit status.
+    A process still running at the timeout is killed with the rest (no rank outlives the test)."""
+    assert os.path.exists(EXE), "build() compiles tests/cpp/bin/co_demo"
+    procs = [subprocess.Popen([EXE] + [str(a) for a in args_of_rank(r)], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(n)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=timeout))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    lines = [json.loads(l) for o, _ in outs for l in o.splitlines() if l.startswith("{")]
+    return [p.returncode for p in procs], lines, "".join(e for _, e in outs)
+
+
+def _shm_name(tag):
+    return f"/ghxt_{tag}_{os.getpid()}"
+
+
+@pytest.mark.parametrize("n", [2, 3, 5])
+def test_shm_transport_all_gather_processes_cpu(n):
+    """include/ghex_amd/shm_transport.hpp's setup collective with ranks as PROCESSES (no GPU
+    calls): 60 all_gather rounds of varying sizes (0..4 KB) with barriers between, every byte of
+    every contribution checked on every rank; the segment is unlinked once all have attached."""
+    name = _shm_name(f"g{n}")
+    rcs, lines, err = _run_procs(lambda r: ["shmgather", name, r, n, 60], n, timeout=60)
+    assert rcs == [0] * n, (lines, err)
+    assert sorted(l["rank"] for l in lines) == list(range(n))
+    assert all(l["bad"] == 0 for l in lines)
+    assert not os.path.exists("/dev/shm" + name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,parts,N,H", [("plain", (2, 1, 1), 10, 2), ("plain", (2, 2, 1), 9, 1),
+                                            ("plain", (1, 1, 2), 10, 2), ("pipe", (2, 2, 1), 8, 2),
+                                            ("pipe", (3, 1, 1), 7, 3)])
+def test_co_shm_processes(mode, parts, N, H):
+    """The C++ communication_object with one PROCESS per rank (shm transport, host-staged
+    messages): one group or per-peer lanes; two fields, two exchanges; every cell of every rank."""
+    n = parts[0] * parts[1] * parts[2]
+    name = _shm_name(f"{mode}{n}")
+    rcs, lines, err = _run_procs(lambda r: ["shm", name, r, *parts, N, H, mode], n)
+    ranks = [l for l in lines if l.get("mode") == "structured"]
+    assert rcs == [0] * n, (lines, err)
+    assert len(ranks) == n and all(l["bad"] == 0 for l in ranks)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,N,H,hosts", [((2, 1, 1), 10, 2, 0), ((2, 2, 1), 8, 2, 0),
+                                             ((2, 2, 2), 6, 3, 0), ((2, 2, 1), 8, 2, 2),
+                                             ((2, 2, 2), 6, 2, 2)])
+def test_co_bulk_device_epochs_processes(parts, N, H, hosts):
+    """The C++ bulk object's device-epoch form (the one it takes when every rank of a host is
+    its own process): IPC puts into the other processes' halos, k_epoch open/close on the
+    object's stream, no host barrier; with emulated hosts the other hosts' halos go through the
+    remote part (a communication_object over the shm transport) in the same exchange().
+    Every cell of every rank, two exchanges; every rank reports device epochs."""
+    n = parts[0] * parts[1] * parts[2]
+    name = _shm_name(f"bulk{n}h{hosts}")
+    rcs, lines, err = _run_procs(lambda r: ["shm", name, r, *parts, N, H, "bulk", hosts], n)
+    ranks = [l for l in lines if l.get("mode") == "bulk"]
+    assert rcs == [0] * n, (lines, err)
+    assert len(ranks) == n
+    assert all(l["bad"] == 0 and l["epochs"] == 1 and l["puts"] >= 1 for l in ranks)
+    assert all(l["remote"] == (1 if hosts else 0) for l in ranks)
