@@ -155,13 +155,21 @@ class shm_transport : public transport
         else
         {
             // the creator may not have got there yet: retry until the name exists at full size
-            wait_until(
-                [&] {
-                    if (fd < 0) fd = shm_open(m_name.c_str(), O_RDWR, 0600);
-                    struct stat st;
-                    return fd >= 0 && fstat(fd, &st) == 0 && std::size_t(st.st_size) == m_total;
-                },
-                "attach (is rank 0 running, with the same name and sizes?)", 0);
+            try
+            {
+                wait_until(
+                    [&] {
+                        if (fd < 0) fd = shm_open(m_name.c_str(), O_RDWR, 0600);
+                        struct stat st;
+                        return fd >= 0 && fstat(fd, &st) == 0 && std::size_t(st.st_size) == m_total;
+                    },
+                    "attach (is rank 0 running, with the same name and sizes?)", 0);
+            }
+            catch (...)
+            {
+                if (fd >= 0) close(fd);
+                throw;
+            }
         }
         void* p = mmap(nullptr, m_total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         close(fd);
@@ -187,7 +195,18 @@ class shm_transport : public transport
                 throw std::runtime_error("shm_transport: rank " + std::to_string(rank) +
                                          " was given other sizes than rank 0");
         }
-        barrier();     // every rank has attached
+        try
+        {
+            barrier();  // every rank has attached
+        }
+        catch (...)
+        {
+            // no destructor runs for a half-built object: leave nothing behind
+            unlink_name();
+            munmap(m_base, m_total);
+            m_base = nullptr;
+            throw;
+        }
         unlink_name();  // nothing left in /dev/shm from here on
     }
     shm_transport(const shm_transport&) = delete;

@@ -34,7 +34,7 @@
 //                                        over IPC with device epochs between the processes;
 //                                        HOSTS > 0 spreads the ranks over emulated hosts, the
 //                                        other hosts' halos through the bulk object's remote part)
-//   co_demo shmgather NAME RANK WORLD ROUNDS
+//   co_demo shmgather NAME RANK WORLD ROUNDS [TIMEOUT_S]
 //                                        the shm transport's all_gather alone (no GPU calls):
 //                                        contributions of varying size, every byte checked
 // Prints one JSON line per rank / result; exit status 0 iff every cell matched.
@@ -420,9 +420,9 @@ int shm_rank(const char* name, int rank, int px, int py, int pz, int N, int H, c
     return run_structured_rank(t, {px, py, pz}, N, H, opt, 2, mode == "bulk", hosts) == 0 ? 0 : 1;
 }
 
-int shm_gather(const char* name, int rank, int world, int rounds)
+int shm_gather(const char* name, int rank, int world, int rounds, double timeout_s)
 {
-    shm_transport t(name, rank, world, std::size_t(1) << 16, 4096);
+    shm_transport t(name, rank, world, std::size_t(1) << 16, 4096, timeout_s);
     long bad = 0;
     for (int round = 0; round < rounds; ++round)
     {
@@ -494,8 +494,9 @@ int main(int argc, char** argv)
         if (mode == "shm" && (argc == 10 || argc == 11))
             return shm_rank(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]),
                             std::atoi(argv[7]), std::atoi(argv[8]), argv[9], argc == 11 ? std::atoi(argv[10]) : 0);
-        if (mode == "shmgather" && argc == 6)
-            return shm_gather(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]));
+        if (mode == "shmgather" && (argc == 6 || argc == 7))
+            return shm_gather(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                              argc == 7 ? std::atof(argv[6]) : 60.0);
     }
     catch (const std::exception& e)
     {

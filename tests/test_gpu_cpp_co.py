@@ -7,6 +7,7 @@ test/unstructured/unstructured_test_case.hpp:345-388: dom*10000 + gid*100 + leve
 import json
 import os
 import subprocess
+import time
 
 import pytest
 
@@ -263,3 +264,16 @@ def test_co_bulk_device_epochs_processes(parts, N, H, hosts):
     assert len(ranks) == n
     assert all(l["bad"] == 0 and l["epochs"] == 1 and l["puts"] >= 1 for l in ranks)
     assert all(l["remote"] == (1 if hosts else 0) for l in ranks)
+
+
+def test_shm_transport_missing_peer_times_out_cpu():
+    """Every wait of the shm transport is bounded: a rank whose peers never start reports an
+    error naming the stage instead of hanging; rank 0 alone leaves no segment behind."""
+    name = _shm_name("lonely")
+    t0 = time.time()
+    rc, lines, err = _run(["shmgather", name, 1, 2, 3, 1.5], timeout=30)
+    assert rc == 2 and "attach" in lines[-1]["error"], (lines, err)
+    rc, lines, err = _run(["shmgather", name, 0, 2, 3, 1.5], timeout=30)
+    assert rc == 2 and "barrier" in lines[-1]["error"], (lines, err)
+    assert time.time() - t0 < 20
+    assert not os.path.exists("/dev/shm" + name)
