@@ -29,6 +29,17 @@ own pack is done and is unpacked as soon as it lands. Device buffers: the native
 serialise the per-peer groups); host staging: per-peer D2H after the pack, host sends as the
 copies land, H2D + unpack per message as it arrives. Peers are issued in one global round-robin
 order on every rank (round_of), which keeps streams that share a hardware queue deadlock-free.
+
+direct=True (node-local peers, device buffers): no transport step at all. Every rank exports its
+peer receive buffers (IPC) at the first exchange of a plan and imports the buffers its peers
+receive into; the ONE pack launch then writes each peer message straight into the receiver's
+buffer (lane-linear 16-B stores: dense writes over xGMI between GPUs, where the bulk object's
+field-to-field puts scatter the x-normal faces' 16-B rows), and the receiver unpacks it locally.
+Ordering is the bulk object's stream-ordered device epochs (libghx ghx_epochs_*; the reference's
+access guards, include/ghex/rma/access_guard.hpp:35-140): k_epoch(open) — this rank's receive
+buffers are free (its previous unpack is done) and every target's are — pack — k_epoch(close) —
+this rank's writes are visible and every source's have landed — unpack. No host synchronisation;
+graph-capturable; structured and unstructured fields alike.
 """
 from __future__ import annotations
 
@@ -137,6 +148,8 @@ class CommunicationHandle:
             self._event.synchronize()
         if co is not None:
             co._valid = False
+            if co.direct:
+                co.check_epochs()
 
     def is_ready(self) -> bool:
         if self._co is not None and self._co.has_scheduled_exchange():
@@ -173,9 +186,17 @@ class CommunicationObject:
     """communication_object<grid, domain_id> (make_communication_object, :1105-1112)."""
 
     def __init__(self, context, fuse_self: bool = True, staging=None, pipelined: bool = False,
-                 rccl_self: bool = False, max_streams: int = 4, copy_engine: str = "probe"):
+                 rccl_self: bool = False, max_streams: int = 4, copy_engine: str = "probe",
+                 direct: bool = False, epoch_timeout: float = 30.0):
         if staging not in (None, "host"):
             raise ValueError("staging must be None (device buffers) or 'host'")
+        if direct and (staging is not None or pipelined or rccl_self):
+            raise ValueError("direct packs into the peers' device buffers: no staging, no "
+                             "pipeline, no rccl_self")
+        # direct: pack straight into node-local peers' receive buffers (module docstring)
+        self.direct = bool(direct)
+        self.epoch_timeout = float(epoch_timeout)
+        self._direct = {}
         if copy_engine not in ("probe", "runtime"):
             raise ValueError("copy_engine must be 'probe' (measured SDMA engines) or 'runtime'")
         # host staging: "probe" = D2H / H2D on the SDMA engines ghex_amd.staging measured,
@@ -364,6 +385,10 @@ class CommunicationObject:
     def _enqueue(self, bis, plan, send, recv, fptrs, sptrs, rptrs, stream):
         import torch
         device = bis[0].field.device
+        if self.direct:
+            d = self._direct_of(plan, send, recv)  # collective at a plan's first exchange
+            if not (self.fuse_self and self.all_self(plan)):
+                return self._exchange_direct(plan, d, fptrs, len(bis), rptrs, len(recv), stream)
         if self.pipelined:
             if self.staging == "host":
                 self._exchange_host_pipelined(plan, send, recv, fptrs, sptrs, rptrs, len(bis),
@@ -600,6 +625,119 @@ class CommunicationObject:
             w.wait()
         for lane in set(lane_of.values()):
             stream.wait_stream(self._peer_stream(lane, device))
+
+    # -- direct: pack into the peers' receive buffers ----------------------------------------
+    def _direct_of(self, plan, send, recv):
+        """Set up a plan's direct exchange (collective: every rank, at the plan's first exchange).
+        Returns {"sptrs": send pointer array with every peer message's entry replaced by the
+        receiver's buffer, "ep": epochs handle or None, "imports": IPC bases}."""
+        d = self._direct.get(id(plan))
+        if d is not None:
+            return d
+        from .bulk_communication_object import hostname
+        me, world = self.context.rank(), self.context.size()
+        host = hostname()
+        mine = []
+        for j, x in enumerate(plan.recv):
+            if x["rank"] == me:
+                continue
+            h = (ctypes.c_ubyte * 64)()
+            off = ctypes.c_uint64()
+            _ghx.call("ghx_ipc_export", ctypes.c_void_p(recv[j].data_ptr()), h, ctypes.byref(off))
+            mine.append((x["rank"], x["tag"], x["size"], bytes(h), off.value))
+        allr = self.context.all_gather_object({"host": host, "recv": mine})
+        ptrs = [t.data_ptr() for t in send]
+        imports = []
+        d = {"sptrs": None, "ep": None, "imports": imports}
+        self._direct[id(plan)] = d  # before anything can raise: __del__ closes what was opened
+        by_peer = {}
+        for i, x in enumerate(plan.send):
+            if x["rank"] != me:
+                by_peer.setdefault(x["rank"], []).append(i)
+        for p, idx in sorted(by_peer.items()):
+            if allr[p]["host"] != host:
+                raise RuntimeError(f"direct exchange: rank {p} is on host {allr[p]['host']!r}, "
+                                   f"not {host!r} (node-local peers only)")
+            # messages of one rank pair: the k-th in tag order on both sides (as route() matches
+            # them; stable sorts keep the plan order among equal tags)
+            theirs = sorted((e for e in allr[p]["recv"] if e[0] == me), key=lambda e: e[1])
+            ours = sorted(idx, key=lambda i: plan.send[i]["tag"])
+            if len(theirs) != len(ours):
+                raise RuntimeError(f"direct exchange: rank {p} expects {len(theirs)} messages "
+                                   f"from rank {me}, which sends {len(ours)}")
+            for i, (_, tag, size, hb, off) in zip(ours, theirs):
+                if tag != plan.send[i]["tag"] or size != plan.send[i]["size"]:
+                    raise RuntimeError(f"direct exchange: message mismatch with rank {p} (tag "
+                                       f"{plan.send[i]['tag']}/{tag}, {plan.send[i]['size']}/{size} B)")
+                base, ptr = ctypes.c_void_p(), ctypes.c_void_p()
+                _ghx.call("ghx_ipc_import", (ctypes.c_ubyte * 64).from_buffer_copy(hb), off,
+                          ctypes.byref(base), ctypes.byref(ptr))
+                imports.append(base.value)
+                ptrs[i] = ptr.value
+        if world > 1:
+            # one node-shared flag block per plan: the lowest rank creates it, the others attach
+            # after an all-gather of the name, the creator unlinks it once all have attached
+            import os
+            import secrets
+            name = f"/ghx_dx_{os.getpid()}_{secrets.token_hex(6)}" if me == 0 else None
+            h = ctypes.c_void_p()
+            if me == 0:  # created (and sized) before anyone learns its name
+                _ghx.call("ghx_epochs_create", name.encode(), 1, world, me, self.epoch_timeout,
+                          ctypes.byref(h))
+                d["ep"] = h
+            names = self.context.all_gather_object(name)
+            if me != 0:
+                _ghx.call("ghx_epochs_create", names[0].encode(), 0, world, me,
+                          self.epoch_timeout, ctypes.byref(h))
+                d["ep"] = h
+            self.context.all_gather_object(None)  # every rank has attached
+            if me == 0:
+                _ghx.call("ghx_epochs_unlink", name.encode())
+            srcs = sorted({x["rank"] for x in plan.recv if x["rank"] != me})
+            tgts = sorted(by_peer)
+            _ghx.call("ghx_epochs_peers", h, _ghx.i32_array(srcs), len(srcs),
+                      _ghx.i32_array(tgts), len(tgts))
+        d["sptrs"] = _ghx.ptr_array(ptrs)
+        return d
+
+    def _exchange_direct(self, plan, d, fptrs, nf, rptrs, nr, stream):
+        s = stream.cuda_stream
+        mixed = self.fuse_self and self.mixed(plan)
+        if d["ep"] is not None:
+            _ghx.call("ghx_epochs_enqueue", d["ep"], 0, s)  # open: buffers free here and there
+        _ghx.call("ghx_exchange_pack_self" if mixed else "ghx_exchange_pack", plan.h, fptrs, nf,
+                  d["sptrs"], len(plan.send), s)
+        if d["ep"] is not None:
+            _ghx.call("ghx_epochs_enqueue", d["ep"], 1, s)  # close: every source's writes landed
+        _ghx.call("ghx_exchange_unpack_peers" if mixed else "ghx_exchange_unpack", plan.h, fptrs,
+                  nf, rptrs, nr, s)
+        import torch
+        if torch.cuda.is_current_stream_capturing():
+            return CommunicationHandle(self, stream, None)  # completion is the graph replay's
+        return CommunicationHandle(self, stream, self._done_event(stream))
+
+    def check_epochs(self):
+        """Raise if a direct exchange's epoch wait timed out (a peer never reached it)."""
+        for d in self._direct.values():
+            if d["ep"] is None:
+                continue
+            err = ctypes.c_int32()
+            _ghx.call("ghx_epochs_status", d["ep"], ctypes.byref(err), None)
+            if err.value:
+                raise RuntimeError(f"direct exchange: an epoch wait timed out after "
+                                   f"{self.epoch_timeout:.0f} s in the "
+                                   f"{'open' if err.value == 1 else 'close'} phase")
+
+    def __del__(self):
+        try:
+            for d in self.__dict__.get("_direct", {}).values():
+                for b in d["imports"]:
+                    _ghx.lib().ghx_ipc_close(ctypes.c_void_p(b))
+                if d["ep"] is not None:
+                    _ghx.lib().ghx_epochs_destroy(d["ep"])
+        except Exception:
+            pass
+        self._direct = {}
 
     # low-level access for benchmarks / tests (no transport)
     def pack_only(self, bis, stream=None):

@@ -6,10 +6,11 @@ MASTER_ADDR / MASTER_PORT in the environment; exits 0 when every cell of the ran
 
 With mode "bulk" the exchange is the zero-copy BulkCommunicationObject instead: every rank puts
 its send regions straight into the peers' fields through IPC mappings (same GPU here, peer
-GPUs over xGMI on a multi-GPU node). Mode "pipe" is the pipelined host-staged exchange (one
+GPUs over xGMI on a multi-GPU node). Modes "direct*": the CommunicationObject's direct form
+(the pack writes into the receivers' buffers through IPC mappings; device epochs). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert]"""
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directrace|directgraph]"""
 import os
 import sys
 
@@ -106,6 +107,45 @@ def main():
             co.check_epochs()
             bad += int(nbad.item())
             continue
+        elif mode in ("direct", "directrace", "directgraph"):
+            # the pack writes every peer message straight into the receiver's buffer (IPC),
+            # device epochs order it; the receiver unpacks locally (no transport step)
+            co = R.make_communication_object(ctx, direct=True, epoch_timeout=60)
+            if mode == "direct":
+                for _ in range(reps):
+                    co.exchange([pc(fd)]).wait()
+            else:
+                # rewrite / exchange / check on the stream with no host synchronisation (race),
+                # or the exchange captured once into a graph and replayed (graph): a pack that
+                # wrote into a buffer its receiver still unpacked from, or an unpack before every
+                # source's writes landed, would leave values of another exchange behind
+                src = torch.from_numpy(a).cuda()
+                exp_d = torch.from_numpy(expect).cuda()
+                co.exchange([pc(fd)]).wait()
+                run = lambda: co.exchange([pc(fd)])
+                if mode == "directgraph":
+                    g = torch.cuda.CUDAGraph()
+                    side = torch.cuda.Stream()
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):
+                        co.exchange([pc(fd)])
+                        co._valid = False
+                    torch.cuda.current_stream().wait_stream(side)
+                    with torch.cuda.graph(g):
+                        co.exchange([pc(fd)])
+                        co._valid = False
+                    run = g.replay
+                nbad = torch.zeros((), dtype=torch.int64, device="cuda")
+                for k in range(4 * reps):
+                    f = float(k % 5 + 1)
+                    base.copy_(src * f)
+                    run()
+                    co._valid = False  # the next exchange is ordered on the stream, not awaited
+                    nbad += (base != exp_d * f).sum()
+                torch.cuda.synchronize()
+                co.check_epochs()
+                bad += int(nbad.item())
+                continue
         elif mode == "sched":  # schedule_exchange on a side stream, host-staged transport
             co = R.make_communication_object(ctx, staging="host")
             s = torch.cuda.Stream()

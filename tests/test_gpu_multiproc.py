@@ -62,14 +62,19 @@ _CASES = [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)]
                          [(_CASES[1][0], _CASES[1][1], _CASES[1][2], m)
                           for m in ("stagedrt", "bulkhost", "bulkmixed", "bulkrace", "bulkgraph",
                                     "pipert")] +
-                         [(_CASES[0][0], _CASES[0][1], _CASES[0][2], "bulkmixed")])
+                         [(_CASES[0][0], _CASES[0][1], _CASES[0][2], "bulkmixed")] +
+                         [(c[0], c[1], c[2], "direct") for c in _CASES] +
+                         [(_CASES[1][0], _CASES[1][1], _CASES[1][2], m)
+                          for m in ("directrace", "directgraph")])
 def test_exchange_multi_process(parts, N, Hw, mode):
     """staged: CommunicationObject(staging="host") over gloo; bulk: zero-copy IPC puts ordered by
     device-side epochs (bulkhost: by host drains + barriers; bulkrace: device epochs as the only
     ordering between rewriting the fields, the exchanges and the halo checks; bulkgraph: the
     exchange captured into a graph and replayed, one epoch per replay; bulkmixed: two emulated
     hosts, puts inside a host and a host-staged buffered exchange between them); pipe: the
-    pipelined host-staged exchange (per-peer streams, send as each copy lands). Host copies on
+    pipelined host-staged exchange (per-peer streams, send as each copy lands); direct: the pack
+    writes into the receivers' buffers through IPC, device epochs, local unpack (directrace /
+    directgraph: ordered on the stream only / replayed from a graph). Host copies on
     the measured SDMA engines (ghex_amd.staging) by default; stagedrt / pipert: hipMemcpyAsync."""
     _run(parts, N, Hw, mode)
 
@@ -78,3 +83,8 @@ def test_pipelined_eight_ranks():
     """The 2x2x2 decomposition (7 peers per rank, every pair once in the round order) with the
     pipelined host-staged exchange, 8 processes on the one GPU."""
     _run((2, 2, 2), 8, 2, "pipe")
+
+
+def test_direct_eight_ranks():
+    """The direct exchange at the 2x2x2 decomposition, 8 processes on the one GPU."""
+    _run((2, 2, 2), 8, 2, "direct")
