@@ -27,6 +27,7 @@
 #pragma once
 
 #include <ghx.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <array>
@@ -315,6 +316,13 @@ struct communication_options
     // (transport::exchange_peer), its buffers unpacked there; peers in the global round order
     bool pipelined = false;
     int max_streams = 4;
+    // direct (one process per rank, node-local peers, device buffers): the pack launch writes
+    // each peer message straight into the receiver's buffer (IPC mapping; xGMI between GPUs),
+    // device epochs (ghx_epochs_*) order it, the receiver unpacks locally — no transport step.
+    // Setup at a plan's first exchange: receive buffers exported and imported over the
+    // transport's all_gather (collective). The Python CommunicationObject(direct=True).
+    bool direct = false;
+    double epoch_timeout = 30.0;  // seconds an epoch wait may take before wait() throws
 };
 
 // communication_object<grid, domain_id> (make_communication_object, :1105-1112)
@@ -338,8 +346,13 @@ class communication_object
         bool fused = false;
         bool mixed = false;  // self AND peer messages: ghx_exchange_pack_self / _unpack_peers
         std::vector<void*> sptr, rptr;
+        std::vector<void*> dsptr;     // direct: peer-message entries = the receivers' buffers
+        ghx_epochs* ep = nullptr;     // direct: this plan's flag block
+        std::vector<void*> imports;   // direct: IPC bases to close
         ~plan()
         {
+            for (auto b : imports) ghx_ipc_close(b);
+            if (ep) ghx_epochs_destroy(ep);
             for (auto* v : {&send, &recv})
                 for (auto& b : *v)
                     if (b.owned && b.data) (void)hipFree(b.data);
@@ -362,6 +375,8 @@ class communication_object
     : m_ctx{&ctx}
     , m_opt{opt}
     {
+        if (m_opt.direct && (m_opt.pipelined || m_opt.self_through_transport))
+            throw std::runtime_error("direct packs into the peers' buffers: no pipeline, no self_through_transport");
         // a non-blocking stream of the greatest priority, like the reference's device::stream
         // (include/ghex/device/cuda/stream.hpp:30-37)
         int lo = 0, hi = 0;
@@ -438,6 +453,7 @@ class communication_object
     {
         check_hip(hipEventSynchronize(m_done), "hipEventSynchronize");
         m_valid = false;
+        check_epochs();
     }
     bool ready()
     {
@@ -445,7 +461,143 @@ class communication_object
         if (e == hipErrorNotReady) return false;
         check_hip(e, "hipEventQuery");
         m_valid = false;
+        check_epochs();
         return true;
+    }
+    void check_epochs() const
+    {
+        for (const auto& kv : m_plans)
+        {
+            if (!kv.second->ep) continue;
+            std::int32_t err = 0;
+            check_ghx(ghx_epochs_status(kv.second->ep, &err, nullptr), "ghx_epochs_status");
+            if (err)
+                throw std::runtime_error(std::string("direct exchange: an epoch wait timed out in the ") +
+                                         (err == 1 ? "open phase (a receiver never freed its buffers)"
+                                                   : "close phase (a sender never completed its pack)"));
+        }
+    }
+
+    // direct: export this rank's peer receive buffers, import the ones its messages go to, and
+    // attach the plan's epoch flag block (collective over the transport, at plan creation)
+    void setup_direct(plan& p)
+    {
+        auto& t = m_ctx->get_transport();
+        const int me = m_ctx->rank(), world = m_ctx->size();
+        char hn[256] = {0};
+        if (gethostname(hn, sizeof(hn) - 1) != 0) hn[0] = '?';
+        const std::string host(hn);
+        std::vector<char> mine;
+        detail::put(mine, std::int32_t(host.size()));
+        mine.insert(mine.end(), host.begin(), host.end());
+        detail::put(mine, std::int64_t(getpid()));
+        std::int32_t n = 0;
+        for (auto& b : p.recv) n += b.rank != me;
+        detail::put(mine, n);
+        for (auto& b : p.recv)
+        {
+            if (b.rank == me) continue;
+            unsigned char h[64];
+            std::uint64_t off = 0;
+            check_ghx(ghx_ipc_export(b.data, h, &off), "ghx_ipc_export");
+            detail::put(mine, b.rank);
+            detail::put(mine, b.tag);
+            detail::put(mine, b.size);
+            mine.insert(mine.end(), reinterpret_cast<char*>(h), reinterpret_cast<char*>(h) + 64);
+            detail::put(mine, off);
+        }
+        const auto all = t.all_gather(mine);
+        struct entry
+        {
+            std::int32_t src, tag;
+            std::uint64_t size, off;
+            unsigned char h[64];
+        };
+        std::vector<std::string> hosts(static_cast<std::size_t>(world));
+        std::vector<std::int64_t> pids(static_cast<std::size_t>(world));
+        std::vector<std::vector<entry>> recv_of(static_cast<std::size_t>(world));
+        for (int r = 0; r < world; ++r)
+        {
+            const auto& in = all[std::size_t(r)];
+            std::size_t pos = 0;
+            const auto hl = detail::get<std::int32_t>(in, pos);
+            if (hl < 0 || pos + std::size_t(hl) > in.size()) throw std::runtime_error("malformed direct payload");
+            hosts[std::size_t(r)].assign(in.data() + pos, std::size_t(hl));
+            pos += std::size_t(hl);
+            pids[std::size_t(r)] = detail::get<std::int64_t>(in, pos);
+            const auto k = detail::get<std::int32_t>(in, pos);
+            for (std::int32_t i = 0; i < k; ++i)
+            {
+                entry e{};
+                e.src = detail::get<std::int32_t>(in, pos);
+                e.tag = detail::get<std::int32_t>(in, pos);
+                e.size = detail::get<std::uint64_t>(in, pos);
+                if (pos + 64 > in.size()) throw std::runtime_error("malformed direct payload");
+                std::memcpy(e.h, in.data() + pos, 64);
+                pos += 64;
+                e.off = detail::get<std::uint64_t>(in, pos);
+                recv_of[std::size_t(r)].push_back(e);
+            }
+        }
+        p.dsptr = p.sptr;
+        std::map<int, std::vector<std::size_t>> by_peer;
+        for (std::size_t i = 0; i < p.send.size(); ++i)
+            if (p.send[i].rank != me) by_peer[p.send[i].rank].push_back(i);
+        for (auto& [q, idx] : by_peer)
+        {
+            if (hosts[std::size_t(q)] != host || pids[std::size_t(q)] == pids[std::size_t(me)])
+                throw std::runtime_error("direct exchange: rank " + std::to_string(q) +
+                                         " is not another process of this host (direct needs one "
+                                         "process per rank, node-local)");
+            // the k-th message of the pair in tag order on both sides (stable: plan order)
+            std::vector<entry> theirs;
+            for (const auto& e : recv_of[std::size_t(q)])
+                if (e.src == me) theirs.push_back(e);
+            std::stable_sort(theirs.begin(), theirs.end(), [](const entry& a, const entry& b) { return a.tag < b.tag; });
+            std::stable_sort(idx.begin(), idx.end(),
+                             [&](std::size_t a, std::size_t b) { return p.send[a].tag < p.send[b].tag; });
+            if (theirs.size() != idx.size())
+                throw std::runtime_error("direct exchange: rank " + std::to_string(q) + " expects " +
+                                         std::to_string(theirs.size()) + " messages, this rank sends " +
+                                         std::to_string(idx.size()));
+            for (std::size_t k = 0; k < idx.size(); ++k)
+            {
+                const auto& b = p.send[idx[k]];
+                const auto& e = theirs[k];
+                if (e.tag != b.tag || e.size != b.size)
+                    throw std::runtime_error("direct exchange: message mismatch with rank " + std::to_string(q));
+                void *base = nullptr, *ptr = nullptr;
+                check_ghx(ghx_ipc_import(e.h, e.off, &base, &ptr), "ghx_ipc_import");
+                p.imports.push_back(base);
+                p.dsptr[idx[k]] = ptr;
+            }
+        }
+        if (world > 1)
+        {
+            std::string name;
+            if (me == 0)  // created (and sized) before anyone learns its name
+            {
+                name = "/ghx_dx_" + std::to_string(getpid()) + "_" +
+                       std::to_string(reinterpret_cast<std::uintptr_t>(&p) & 0xffffffu);
+                check_ghx(ghx_epochs_create(name.c_str(), 1, world, me, m_opt.epoch_timeout, &p.ep),
+                          "ghx_epochs_create");
+            }
+            const auto names = t.all_gather(std::vector<char>(name.begin(), name.end()));
+            if (me != 0)
+                check_ghx(ghx_epochs_create(std::string(names[0].begin(), names[0].end()).c_str(), 0, world, me,
+                                            m_opt.epoch_timeout, &p.ep),
+                          "ghx_epochs_create");
+            (void)t.all_gather({});  // every rank has attached
+            if (me == 0) (void)ghx_epochs_unlink(name.c_str());
+            std::vector<std::int32_t> srcs, tgts;
+            for (auto& b : p.recv)
+                if (b.rank != me && std::find(srcs.begin(), srcs.end(), b.rank) == srcs.end()) srcs.push_back(b.rank);
+            for (auto& kv : by_peer) tgts.push_back(kv.first);
+            std::sort(srcs.begin(), srcs.end());
+            check_ghx(ghx_epochs_peers(p.ep, srcs.data(), std::int32_t(srcs.size()), tgts.data(),
+                                       std::int32_t(tgts.size())),
+                      "ghx_epochs_peers");
+        }
     }
 
     // tag offsets per distinct pattern container in argument order (:540-549) are assigned in
@@ -585,6 +737,7 @@ class communication_object
             p->fused = false;
             p->mixed = false;
         }
+        if (m_opt.direct) setup_direct(*p);  // every rank, at this plan's first exchange
         auto& ref = *p;
         m_plans.emplace(std::move(key), std::move(p));
         return ref;
@@ -668,6 +821,24 @@ class communication_object
             run_pipelined(p, fptrs, nf, ns, nr);
         else if (p.fused)
             check_ghx(ghx_exchange_self(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream), "ghx_exchange_self");
+        else if (m_opt.direct)
+        {
+            // open (buffers free here and at every receiver) -> pack into the receivers'
+            // buffers -> close (every sender's pack landed) -> local unpack
+            if (p.ep) check_ghx(ghx_epochs_enqueue(p.ep, 0, m_stream), "ghx_epochs_enqueue(open)");
+            if (p.mixed)
+                check_ghx(ghx_exchange_pack_self(p.ex, fptrs.data(), nf, p.dsptr.data(), ns, m_stream),
+                          "ghx_exchange_pack_self");
+            else
+                check_ghx(ghx_exchange_pack(p.ex, fptrs.data(), nf, p.dsptr.data(), ns, m_stream), "ghx_exchange_pack");
+            if (p.ep) check_ghx(ghx_epochs_enqueue(p.ep, 1, m_stream), "ghx_epochs_enqueue(close)");
+            if (p.mixed)
+                check_ghx(ghx_exchange_unpack_peers(p.ex, fptrs.data(), nf, p.rptr.data(), nr, m_stream),
+                          "ghx_exchange_unpack_peers");
+            else
+                check_ghx(ghx_exchange_unpack(p.ex, fptrs.data(), nf, p.rptr.data(), nr, m_stream),
+                          "ghx_exchange_unpack");
+        }
         else
         {
             if (p.mixed)  // the pack launch also completes the self messages

@@ -30,7 +30,9 @@
 //   co_demo shm NAME RANK PX PY PZ N H MODE [HOSTS]
 //                                        ONE rank of a PX*PY*PZ job, this process (start one
 //                                        process per rank; shm_transport NAME): MODE plain (one
-//                                        group), pipe (per-peer lanes) or bulk (zero-copy puts
+//                                        group), pipe (per-peer lanes), direct (the pack writes
+//                                        into the receivers' buffers over IPC, device epochs) or
+//                                        bulk (zero-copy puts
 //                                        over IPC with device epochs between the processes;
 //                                        HOSTS > 0 spreads the ranks over emulated hosts, the
 //                                        other hosts' halos through the bulk object's remote part)
@@ -410,13 +412,15 @@ int rma_case(int n)
 int shm_rank(const char* name, int rank, int px, int py, int pz, int N, int H, const std::string& mode,
              int hosts)
 {
-    if (mode != "plain" && mode != "pipe" && mode != "bulk") throw std::runtime_error("MODE: plain|pipe|bulk");
+    if (mode != "plain" && mode != "pipe" && mode != "bulk" && mode != "direct")
+        throw std::runtime_error("MODE: plain|pipe|bulk|direct");
     const int n = px * py * pz;
     // channels sized for the largest message group of the test geometries (two fields)
     const std::size_t face = std::size_t(N + 2 * H) * std::size_t(N + 2 * H) * std::size_t(H) * 12;
     shm_transport t(name, rank, n, std::size_t(1) << 20, 8 + 26 * (16 + 8) + 26 * face);
     communication_object::options opt;
     opt.pipelined = mode == "pipe";
+    opt.direct = mode == "direct";
     return run_structured_rank(t, {px, py, pz}, N, H, opt, 2, mode == "bulk", hosts) == 0 ? 0 : 1;
 }
 

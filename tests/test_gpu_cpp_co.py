@@ -234,10 +234,14 @@ def test_shm_transport_all_gather_processes_cpu(n):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,parts,N,H", [("plain", (2, 1, 1), 10, 2), ("plain", (2, 2, 1), 9, 1),
                                             ("plain", (1, 1, 2), 10, 2), ("pipe", (2, 2, 1), 8, 2),
-                                            ("pipe", (3, 1, 1), 7, 3)])
+                                            ("pipe", (3, 1, 1), 7, 3), ("direct", (2, 1, 1), 10, 2),
+                                            ("direct", (2, 2, 1), 8, 3), ("direct", (1, 1, 2), 9, 1),
+                                            ("direct", (2, 2, 2), 6, 2)])
 def test_co_shm_processes(mode, parts, N, H):
     """The C++ communication_object with one PROCESS per rank (shm transport, host-staged
-    messages): one group or per-peer lanes; two fields, two exchanges; every cell of every rank."""
+    messages): one group or per-peer lanes; or direct (options.direct: the pack writes into the
+    receivers' buffers over IPC, device epochs, no transport step); two fields (double + float:
+    mixed pads), two exchanges; every cell of every rank."""
     n = parts[0] * parts[1] * parts[2]
     name = _shm_name(f"{mode}{n}")
     rcs, lines, err = _run_procs(lambda r: ["shm", name, r, *parts, N, H, mode], n)
