@@ -10,7 +10,8 @@ GPUs over xGMI on a multi-GPU node). Modes "direct*": the CommunicationObject's 
 (the pack writes into the receivers' buffers through IPC mappings; device epochs). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directrace|directgraph]"""
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directrace|directgraph|udirect]
+(udirect: <px> <py> <pz> = world split, <N> = cells per rank, <H> = levels)"""
 import os
 import sys
 
@@ -34,6 +35,8 @@ def main():
     from tests import helpers as H
     from tests.gpu_util import device_field
     ghex_amd.native_library()
+    if mode == "udirect":
+        sys.exit(unstructured_direct(rank, world, N, Hw, reps))
     ranks, gf, gl = H.cube_domains(N, (px, py, pz))
     dom = ranks[rank][0]
     ctx = ghex_amd.make_context()
@@ -181,6 +184,50 @@ def main():
     del co
     dist.destroy_process_group()
     sys.exit(0 if int(t.item()) == 0 else 1)
+
+
+def unstructured_direct(rank, world, cells, levels, reps):
+    """Mode udirect: an unstructured exchange through CommunicationObject(direct=True) between
+    the processes — every rank owns `cells` cells (gids rank*10^6 + i) and holds cells/4 halo
+    cells drawn from the other ranks, in a random storage order, `levels` levels (levels first);
+    value(gid, level) = gid*100 + level; every halo value checked after each exchange."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import ghex_amd
+    from ghex_amd import unstructured as U
+    rng = np.random.default_rng(4242 + rank)
+    nh = cells // 4
+    others = np.array([r for r in range(world) if r != rank])
+    owner = others[rng.integers(0, len(others), size=4 * nh)]
+    halo = np.unique(owner.astype(np.int64) * 1_000_000 + rng.integers(0, cells, size=4 * nh))
+    halo = rng.permutation(halo)[:nh]
+    gids = np.concatenate([rank * 1_000_000 + np.arange(cells, dtype=np.int64), halo])
+    perm = rng.permutation(len(gids))
+    gids = gids[perm]
+    outer = np.nonzero(perm >= cells)[0]
+    ctx = ghex_amd.make_context()
+    dd = U.DomainDescriptor(rank, gids.tolist(), outer.tolist())
+    pc = U.make_pattern(ctx, U.HaloGenerator(), [dd])
+    want = gids.astype(np.float64)[:, None] * 100.0 + np.arange(levels)[None, :]
+    init = want.copy()
+    init[outer] = -1.0
+    field = torch.from_numpy(init).cuda()  # (cells, levels): levels fastest
+    fd = U.make_field_descriptor(dd, field)
+    co = U.make_communication_object(ctx, direct=True, epoch_timeout=60)
+    bad = 0
+    for _ in range(reps):
+        field[torch.from_numpy(outer).cuda()] = -1.0
+        co.exchange([pc(fd)]).wait()
+        bad += int(np.count_nonzero(field.cpu().numpy() != want))
+    t = torch.tensor([bad])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(f"udirect world {world} cells {cells} levels {levels}: bad cells {int(t.item())}")
+    dist.barrier()
+    del co
+    dist.destroy_process_group()
+    return 0 if int(t.item()) == 0 else 1
 
 
 if __name__ == "__main__":

@@ -88,3 +88,10 @@ def test_pipelined_eight_ranks():
 def test_direct_eight_ranks():
     """The direct exchange at the 2x2x2 decomposition, 8 processes on the one GPU."""
     _run((2, 2, 2), 8, 2, "direct")
+
+
+@pytest.mark.parametrize("world,levels", [(2, 1), (4, 3)])
+def test_direct_unstructured(world, levels):
+    """The direct exchange of an unstructured field (random storage order, halo cells drawn from
+    every other rank, levels first): the same plan machinery as the structured one."""
+    _run((world, 1, 1), 3000, levels, "udirect")
