@@ -98,6 +98,31 @@ def route(context, sends, recvs, group=None):
     return dist.batch_isend_irecv(ops)
 
 
+def direct_matches(me, send, recv_of):
+    """The direct exchange's message matching: for each of this rank's peer send buffers
+    (`send`: the plan's send dicts) the receiver's published entry (src, tag, size, ...) from
+    `recv_of[peer]`. Messages of one rank pair match k-th to k-th in tag order on both sides, as
+    route() matches them (stable sorts keep the plan order among equal tags); counts, tags and
+    sizes must agree. Returns [(send index, entry)]."""
+    by_peer = {}
+    for i, x in enumerate(send):
+        if x["rank"] != me:
+            by_peer.setdefault(x["rank"], []).append(i)
+    out = []
+    for p, idx in sorted(by_peer.items()):
+        theirs = sorted((e for e in recv_of[p] if e[0] == me), key=lambda e: e[1])
+        ours = sorted(idx, key=lambda i: send[i]["tag"])
+        if len(theirs) != len(ours):
+            raise RuntimeError(f"direct exchange: rank {p} expects {len(theirs)} messages "
+                               f"from rank {me}, which sends {len(ours)}")
+        for i, e in zip(ours, theirs):
+            if e[1] != send[i]["tag"] or e[2] != send[i]["size"]:
+                raise RuntimeError(f"direct exchange: message mismatch with rank {p} (tag "
+                                   f"{send[i]['tag']}/{e[1]}, {send[i]['size']}/{e[2]} B)")
+            out.append((i, e))
+    return out
+
+
 def round_of(a: int, b: int, world: int) -> int:
     """Round of the pair (a, b) in a round-robin tournament over `world` ranks (circle method):
     every rank meets every other rank exactly once, each rank in at most one pair per round.
@@ -654,26 +679,17 @@ class CommunicationObject:
         for i, x in enumerate(plan.send):
             if x["rank"] != me:
                 by_peer.setdefault(x["rank"], []).append(i)
-        for p, idx in sorted(by_peer.items()):
+        for p in by_peer:
             if allr[p]["host"] != host:
                 raise RuntimeError(f"direct exchange: rank {p} is on host {allr[p]['host']!r}, "
                                    f"not {host!r} (node-local peers only)")
-            # messages of one rank pair: the k-th in tag order on both sides (as route() matches
-            # them; stable sorts keep the plan order among equal tags)
-            theirs = sorted((e for e in allr[p]["recv"] if e[0] == me), key=lambda e: e[1])
-            ours = sorted(idx, key=lambda i: plan.send[i]["tag"])
-            if len(theirs) != len(ours):
-                raise RuntimeError(f"direct exchange: rank {p} expects {len(theirs)} messages "
-                                   f"from rank {me}, which sends {len(ours)}")
-            for i, (_, tag, size, hb, off) in zip(ours, theirs):
-                if tag != plan.send[i]["tag"] or size != plan.send[i]["size"]:
-                    raise RuntimeError(f"direct exchange: message mismatch with rank {p} (tag "
-                                       f"{plan.send[i]['tag']}/{tag}, {plan.send[i]['size']}/{size} B)")
-                base, ptr = ctypes.c_void_p(), ctypes.c_void_p()
-                _ghx.call("ghx_ipc_import", (ctypes.c_ubyte * 64).from_buffer_copy(hb), off,
-                          ctypes.byref(base), ctypes.byref(ptr))
-                imports.append(base.value)
-                ptrs[i] = ptr.value
+        for i, (_, tag, size, hb, off) in direct_matches(me, plan.send,
+                                                         {r: a["recv"] for r, a in enumerate(allr)}):
+            base, ptr = ctypes.c_void_p(), ctypes.c_void_p()
+            _ghx.call("ghx_ipc_import", (ctypes.c_ubyte * 64).from_buffer_copy(hb), off,
+                      ctypes.byref(base), ctypes.byref(ptr))
+            imports.append(base.value)
+            ptrs[i] = ptr.value
         if world > 1:
             # one node-shared flag block per plan: the lowest rank creates it, the others attach
             # after an all-gather of the name, the creator unlinks it once all have attached
