@@ -282,6 +282,16 @@ def bulk_child(args):
     bco.check_epochs()
     Tw = timed(lambda: bco.exchange().wait(), k)
     n = E ** 3 - N ** 3
+    line = {"isolated": True, "verified": bad.item() == 0,
+            "exchange_ms_per_step": round(T / k * 1e3, 4),
+            "exchange_wait_ms_per_step": round(Tw / k * 1e3, 4),
+            "GBps_moved": round(world * 2 * n * 8 * k / T / 1e9, 1),
+            "epochs": bco.epochs, "put_launches": len(bco._puts),
+            "bytes_moved_per_step_per_gpu": 2 * n * 8,
+            "transport": "IPC puts into the peers' fields (over xGMI between GPUs), device epochs; "
+                         "gloo for setup only"}
+    if rank == 0:  # the puts' result, in case the direct leg below never returns
+        print(json.dumps(dict(line, direct={"error": "did not finish"})), flush=True)
     # the direct exchange (CommunicationObject(direct=True)): the pack writes each peer message
     # into the receiver's buffer over xGMI (IPC), device epochs, local unpack; halos reset first
     direct = {}
@@ -314,15 +324,7 @@ def bulk_child(args):
     except Exception as e:  # reported in the line, never fatal for the bulk leg
         direct = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
     if rank == 0:
-        print(json.dumps({"isolated": True, "verified": bad.item() == 0, "direct": direct,
-                          "exchange_ms_per_step": round(T / k * 1e3, 4),
-                          "exchange_wait_ms_per_step": round(Tw / k * 1e3, 4),
-                          "GBps_moved": round(world * 2 * n * 8 * k / T / 1e9, 1),
-                          "epochs": bco.epochs, "put_launches": len(bco._puts),
-                          "bytes_moved_per_step_per_gpu": 2 * n * 8,
-                          "transport": "IPC puts into the peers' fields (over xGMI between GPUs), "
-                                       "device epochs; gloo for setup only"}),
-              flush=True)
+        print(json.dumps(dict(line, direct=direct)), flush=True)
     del bco
     dist.barrier()
     dist.destroy_process_group()
@@ -355,7 +357,12 @@ def bulk_isolated(args, rank, world, local, port_of_rank0, timeout):
             os.killpg(p.pid, signal.SIGKILL)
         except OSError:
             pass
-        p.communicate()
+        so, _ = p.communicate()
+        lines = [l for l in (so or "").splitlines() if l.startswith("{")]
+        if rank == 0 and lines:  # the puts finished, the direct leg did not
+            res = json.loads(lines[-1])
+            res["error"] = f"timed out after {timeout:.0f} s (after the puts' result)"
+            return res
         return {"isolated": True, "error": f"timed out after {timeout:.0f} s"}
     if p.returncode != 0:
         return {"isolated": True, "error": f"exit {p.returncode}: {se.strip()[-300:]}"}
