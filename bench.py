@@ -66,6 +66,10 @@ def parse():
                         "grid and would mix into a profiler's per-kernel averages)")
     p.add_argument("--bulk-child", action="store_true",
                    help="internal: the isolated zero-copy leg's rank process (see bulk_isolated)")
+    p.add_argument("--bulk-only", type=int, default=0, metavar="N",
+                   help="developer: run only the N>1 isolated zero-copy leg — N --bulk-child "
+                        "processes (puts + direct, verified), spread over the visible GPUs (all "
+                        "on cuda:0 on a one-GPU box), without the headline ranks; rank 0's line")
     p.add_argument("--bulk-timeout", type=float, default=120.0,
                    help="seconds the isolated zero-copy leg (N>1) may take before it is killed")
     p.add_argument("--bulk", action="store_true",
@@ -222,6 +226,21 @@ class Runner:
             self.graphs[k % self.G].replay()
 
 
+def verify_replay(torch, dev, replay, clear, count_bad, send, recv, deliver=None):
+    """Wrong cells after the TIMED kernels alone: halos reset (clear), every send/recv buffer
+    byte set to 0xFF (an fp64 NaN, unequal to every expected value), the timed graph replayed
+    (replay), then — where peer messages exist — deliver() moves the packed send buffers to the
+    receivers and unpacks them; count_bad() checks every cell (summed over ranks)."""
+    clear()
+    for t in list(send) + list(recv):
+        t.fill_(255)
+    replay()
+    if deliver is not None:
+        deliver()
+    torch.cuda.synchronize(dev)
+    return count_bad()
+
+
 def bulk_child(args):
     """One rank of the isolated zero-copy leg (spawned by bulk_isolated, one process per rank,
     the parent rank's GPU): the same domain and field as the headline, exchanged by
@@ -330,6 +349,41 @@ def bulk_child(args):
     dist.destroy_process_group()
 
 
+def bulk_only(args) -> int:
+    """`bench.py --bulk-only N`: the isolated zero-copy leg of an N-GPU run on its own — N
+    --bulk-child processes (each builds its rank's domain, exchanges by IPC puts and then by the
+    direct exchange, verifies every cell), spawned by this process, which never touches the GPU.
+    Rank r runs on GPU r mod (visible GPUs): on a one-GPU box all N share cuda:0, which keeps an
+    N=8 rehearsal at 8 processes on the card (the headline ranks are not started). Prints rank
+    0's line (with n_procs and the GPUs used); exits 0 only when every child did and both forms
+    verified."""
+    import socket
+    import torch  # device_count() does not initialise the GPU on this image
+    n = args.bulk_only
+    if n not in DECOMP or n < 2:
+        raise SystemExit("--bulk-only takes 2, 4 or 8")
+    ngpu = max(1, torch.cuda.device_count())
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(n) as ex:
+        futs = [ex.submit(bulk_isolated, args, r, n, r % ngpu, port, args.bulk_timeout)
+                for r in range(n)]
+        res = [f.result() for f in futs]
+    line = dict(res[0] or {"isolated": True, "error": "rank 0 gave no result"})
+    errs = {r: x["error"] for r, x in enumerate(res) if isinstance(x, dict) and "error" in x}
+    if errs:
+        line["errors"] = errs
+    line.update(mode="bulk-only", n_procs=n, gpus_used=min(n, ngpu),
+                config={"N": args.N, "halo": args.halo, "decomposition": list(DECOMP[n])})
+    print(json.dumps(line), flush=True)
+    ok = (not errs and line.get("verified") is True and
+          line.get("direct", {}).get("verified") is True)
+    return 0 if ok else 1
+
+
 def bulk_isolated(args, rank, world, local, port_of_rank0, timeout):
     """The zero-copy exchange between GPUs, run in child processes (one per rank, spawned, not
     exec'd) so that whatever happens there — a fault, a hang past --bulk-timeout — cannot take
@@ -376,6 +430,8 @@ def main():
     args = parse()
     if args.bulk_child:
         return bulk_child(args)
+    if args.bulk_only:
+        sys.exit(bulk_only(args))  # before anything touches the GPU
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_workers(args))  # before anything touches the GPU
     import threading
@@ -552,12 +608,35 @@ def main():
     dev_time = {}
     T = timed(lambda: runner.run(K), 1, events=True, box=dev_time)
     dev_step = dev_time["s"] / K  # device time per step over the timed region (HIP events)
+    # `verified` refers to the kernels just timed: halos back to -1, every buffer byte to 0xFF,
+    # the timed graph replayed once (N>1: then the peer messages' transport and an unpack), every
+    # cell checked. The first exchange above (at N=1 the fused k_self) is `verified_fused`.
+    verified_fused = verified
+    me = rank
+    t_sends = [(x["rank"], x["tag"], send[i][:x["size"]]) for i, x in enumerate(plan.send)
+               if x["rank"] != me]
+    t_recvs = [(x["rank"], x["tag"], recv[i][:x["size"]]) for i, x in enumerate(plan.recv)
+               if x["rank"] != me]
+
+    def transport_unpack():
+        """Deliver the send buffers the replay packed, then unpack them (N>1)."""
+        from ghex_amd.communication_object import route
+        if args.rehearse:
+            co._exchange_host_staged(plan, t_sends, t_recvs, stream)
+        else:
+            for w in route(ctx, t_sends, t_recvs):
+                w.wait()
+        unpack(stream.cuda_stream)
+
+    with guard.stage("verify_timed", args.exchange_timeout):
+        verified = verify_replay(torch, dev, lambda: runner.run(K), clear_halos, verify,
+                                 send, recv, transport_unpack if t_recvs else None) == 0
     value = world * step_bytes * K / T / 1e9
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": K, "warmup": W, "ms_per_step": round(T / K * 1e3, 5),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (owned cell = global linear index; verified after a full exchange)",
+        "data": "synthetic (owned cell = global linear index; halos -1 before every verification)",
         "config": {
             "workload": f"{N}^3 fp64 structured 3D halo={Hw}, 26-neighbour periodic, "
                         f"device-resident pack+unpack, decomposition {list(parts)}",
@@ -570,6 +649,14 @@ def main():
             "world_size": world, "backend": backend,
         },
         "verified": verified,
+        "verified_what": "the timed hipGraph (k_copy pack + k_copy unpack) replayed once after "
+                         "the timed region on halos reset to -1 and buffers set to 0xFF" +
+                         ("" if world == 1 else ", then transport + unpack") +
+                         "; every cell of every rank checked",
+        "verified_fused": verified_fused,
+        "verified_fused_what": ("the first exchange: co.exchange() = the fused k_self launch"
+                                if world == 1 and co.fuse_self and co.all_self(plan) else
+                                "the first exchange: co.exchange() = pack, transport, unpack"),
     }
     if args.rehearse:
         out["rehearsal"] = ("all ranks on cuda:0, gloo + host-staged transport: code-path check, "
@@ -707,6 +794,18 @@ def extras(args, torch, dist, dev, stream, out, v):
         # the step as an application runs it after a stencil sweep: flush, then pack and unpack
         # back to back (the unpack's halo lines are the ones the pack has just fetched; flushed
         # separately, each launch above pays its own misses)
+        # the same cold launches by the kernels' own events (like pack_kernel_us): what the
+        # launch itself takes after the flush, without the deferred write-back the differenced
+        # figures above charge to it
+        _ghx_ = v["_ghx"]
+        (kpc,) = cold_launch_durations(torch, dev, stream, _ghx_, [pack], clean)
+        (kuc,) = cold_launch_durations(torch, dev, stream, _ghx_, [unpack], clean)
+        kspc, ksuc = cold_launch_durations(torch, dev, stream, _ghx_, [pack, unpack], clean)
+        roof["cold_clean_kernel_events_us"] = {
+            "pack": round(kpc * 1e6, 2), "unpack": round(kuc * 1e6, 2),
+            "step_pack": round(kspc * 1e6, 2), "step_unpack": round(ksuc * 1e6, 2),
+            "method": "flush, then the launch(es) with hipExtLaunchKernel start/stop events, "
+                      "medians of 15; step_*: flush, pack, unpack"}
         t_sc = cold_duration(torch, dev, stream, lambda s: (pack(s), unpack(s)), clean)
         roof["cold_clean_step_us"] = round(t_sc * 1e6, 2)
         roof["cold_clean_step_GBps"] = round(step_bytes / t_sc / 1e9, 1)
@@ -942,7 +1041,7 @@ def fused_floor(N, Hw, launch_us):
         if rc:
             return {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
         return {"floor_us": round(us[0], 2), "floor_cold_us": round(us[1], 2),
-                "k_self_vs_floor": round(us[0] / launch_us, 3) if launch_us else None}
+                "floor_over_kernel": round(us[0] / launch_us, 3) if launch_us else None}
     except Exception as e:  # reported, never fatal
         return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
 
@@ -953,7 +1052,8 @@ def pack_read_floor(N, Hw, roof):
     16-B vector from each 128-B field line the pack must read (x-face lines first, as the pack
     dispatches them) and stream the buffer writes. Unpack ("write_floor"): a kernel that streams
     the buffer in and writes each halo row's bytes once (16-B pieces where aligned). Timed like
-    pack_kernel_us (the kernel's own begin/end events, medians); *_vs_floor = floor / kernel."""
+    pack_kernel_us (the kernel's own begin/end events, medians). floor_over_kernel = floor time /
+    kernel time: above 1 the kernel is FASTER than its probe, below 1 slower."""
     import ctypes
     try:
         L = _floor_lib()
@@ -969,7 +1069,7 @@ def pack_read_floor(N, Hw, roof):
                "reads_us": round(us[4], 2), "reads_writes_us": round(us[6], 2),
                "reads_writes_cold_us": round(us[7], 2),
                "pack_kernel_us": roof.get("pack_kernel_us"),
-               "pack_vs_floor": round(us[6] / roof["pack_kernel_us"], 3)
+               "floor_over_kernel": round(us[6] / roof["pack_kernel_us"], 3)
                if roof.get("pack_kernel_us") else None}
         rc = L.ghx_probe_unpack_floor(N, Hw, 21, us, c)
         if rc:
@@ -981,7 +1081,7 @@ def pack_read_floor(N, Hw, roof):
                 "writes_us": round(us[4], 2), "writes_reads_us": round(us[6], 2),
                 "writes_reads_cold_us": round(us[7], 2),
                 "unpack_kernel_us": roof.get("unpack_kernel_us"),
-                "unpack_vs_floor": round(us[6] / roof["unpack_kernel_us"], 3)
+                "floor_over_kernel": round(us[6] / roof["unpack_kernel_us"], 3)
                 if roof.get("unpack_kernel_us") else None}
         return out
     except Exception as e:  # reported, never fatal
@@ -1069,6 +1169,35 @@ def launch_durations(torch, dev, stream, _ghx, fns, reps=41):
     _ghx.call("ghx_launch_timing", 1)
     try:
         for _ in range(reps):
+            for f in fns:
+                f(s)
+        _ghx.call("ghx_launch_timing_read", ms, n, ctypes.byref(got))
+    finally:
+        _ghx.call("ghx_launch_timing", 0)
+    if got.value != n:
+        return (0.0,) * len(fns)
+    per = [sorted(ms[i::len(fns)]) for i in range(len(fns))]
+    return tuple(p[len(p) // 2] * 1e-3 for p in per)
+
+
+def cold_launch_durations(torch, dev, stream, _ghx, fns, flush, reps=15):
+    """Like launch_durations, each step preceded by flush(s) (a torch kernel, not timed): the
+    kernels' own start/stop events right after a cache flush, medians. Unlike cold_duration (a
+    graph difference), this excludes the write-back of the lines a launch leaves dirty, which
+    the NEXT flush pays."""
+    import ctypes
+    s = stream.cuda_stream
+    flush(s)
+    for f in fns:
+        f(s)
+    torch.cuda.synchronize(dev)
+    n = reps * len(fns)
+    ms = (ctypes.c_float * n)()
+    got = ctypes.c_int32()
+    _ghx.call("ghx_launch_timing", 1)
+    try:
+        for _ in range(reps):
+            flush(s)
             for f in fns:
                 f(s)
         _ghx.call("ghx_launch_timing_read", ms, n, ctypes.byref(got))
@@ -1195,15 +1324,25 @@ def bench_halo(h, v, torch, dist, dev, stream, args, x_alloc=None):
     fd = R.make_field_descriptor(dd, base.permute(2, 1, 0), (h,) * 3, (E,) * 3)
     co = R.make_communication_object(v["ctx"], staging="host" if args.rehearse else None)
     bis = [pc(fd)]
-    co.exchange(bis).wait()
+    interior = base[h:h + N, h:h + N, h:h + N].clone()
     w = [((torch.arange(E, device=dev) - h + first[d]) % G[d]).to(torch.float64) for d in range(3)]
-    bad = int((base != w[0].view(1, 1, E) + G[0] * (w[1].view(1, E, 1) + G[1] *
-                                                     w[2].view(E, 1, 1))).sum().item())
-    if world > 1:
-        t = torch.tensor([float(bad)], dtype=torch.float64,
-                         device="cpu" if args.rehearse else dev)
-        dist.all_reduce(t)
-        bad = int(t.item())
+
+    def count_bad():
+        bad = int((base != w[0].view(1, 1, E) + G[0] * (w[1].view(1, E, 1) + G[1] *
+                                                         w[2].view(E, 1, 1))).sum().item())
+        if world > 1:
+            t = torch.tensor([float(bad)], dtype=torch.float64,
+                             device="cpu" if args.rehearse else dev)
+            dist.all_reduce(t)
+            bad = int(t.item())
+        return bad
+
+    def clear():
+        base.fill_(-1.0)
+        base[h:h + N, h:h + N, h:h + N] = interior
+
+    co.exchange(bis).wait()
+    bad_fused = count_bad()  # the first exchange (N=1: the fused k_self launch)
     plan = co.plan(bis)
     send, recv = co.buffers(plan, dev)
     fptr = _ghx.ptr_array([fd.data_ptr()])
@@ -1228,6 +1367,23 @@ def bench_halo(h, v, torch, dist, dev, stream, args, x_alloc=None):
     # wall time, where one scheduling hiccup of the host moved the figure by 25 % between boxes)
     Ts = sorted(v["timed"](lambda: runner.run(K), 1) for _ in range(5))
     T = Ts[len(Ts) // 2]
+    me = rank
+    t_sends = [(x["rank"], x["tag"], send[i][:x["size"]]) for i, x in enumerate(plan.send)
+               if x["rank"] != me]
+    t_recvs = [(x["rank"], x["tag"], recv[i][:x["size"]]) for i, x in enumerate(plan.recv)
+               if x["rank"] != me]
+
+    def deliver():
+        from ghex_amd.communication_object import route
+        if args.rehearse:
+            co._exchange_host_staged(plan, t_sends, t_recvs, stream)
+        else:
+            for wk in route(v["ctx"], t_sends, t_recvs):
+                wk.wait()
+        unpack(stream.cuda_stream)
+    # `verified`: the timed graph itself (k_copy pack + unpack), replayed on reset halos/buffers
+    bad = verify_replay(torch, dev, lambda: runner.run(K), clear, count_bad, send, recv,
+                        deliver if t_recvs else None)
     t_p, t_u = kernel_durations(torch, dev, stream, [pack, unpack])
     k_p, k_u = launch_durations(torch, dev, stream, _ghx, [pack, unpack])
     n = E ** 3 - N ** 3
@@ -1237,10 +1393,10 @@ def bench_halo(h, v, torch, dist, dev, stream, args, x_alloc=None):
            "pack_us": round(t_p * 1e6, 2),
            "unpack_us": round(t_u * 1e6, 2), "pack_kernel_us": round(k_p * 1e6, 2),
            "unpack_kernel_us": round(k_u * 1e6, 2), "bytes_per_step_per_gpu": 4 * n * 8,
-           "verified": bad == 0}
+           "verified": bad == 0, "verified_fused": bad_fused == 0}
     if x_alloc:
         out["row_pitch_bytes"] = 8 * x_alloc
-    del runner, co, base, alloc, fd, bis, send, recv
+    del runner, co, base, alloc, fd, bis, send, recv, interior, t_sends, t_recvs
     torch.cuda.empty_cache()
     if world == 1 and not x_alloc:
         out["read_floor"] = pack_read_floor(N, h, out)
@@ -1454,10 +1610,89 @@ def _pin(core):
         return False
 
 
+def _median_of_25(times):
+    """25 iterations, the first 5 dropped, the median of the other 20."""
+    t = sorted(times[5:25])
+    return t[len(t) // 2] if t else None
+
+
+def _cpu_quota():
+    """Cores granted by the cgroup's CPU quota (cgroup v2 cpu.max, or v1 cfs quota); None when
+    unlimited or unreadable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // per)
+    except (OSError, ValueError):
+        return None
+
+
+def _mem_available():
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                return int(line.split()[1]) * 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
+# host memory the CPU-baseline ranks may hold together: the GPU box caps one command at about
+# 270 GiB of host RAM (the bench process and torch hold the rest)
+CPU_RANKS_MEM_BUDGET = 128 << 30
+
+
+def cpu_rank_count(share, per_rank_bytes, env=None, quota=None, avail=None):
+    """How many independent single-thread ranks the CPU baseline runs, and why: one per core of
+    this process's affinity set (`nproc` ranks), capped by the cgroup CPU quota,
+    by the box's declared per-GPU CPU share (OMP_NUM_THREADS: the GPU box sets it to the cores a
+    one-GPU job owns and asks that worker pools stay within it) and by host memory (each rank
+    holds its own field). Returns (ranks, [reasons for every cap that bound])."""
+    env = os.environ if env is None else env
+    n = max(1, len(share))
+    caps = [(n, f"affinity set {n} cores")]
+    if quota:
+        caps.append((quota, f"cgroup CPU quota {quota} cores"))
+    try:
+        omp = int(env.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        omp = 0
+    if omp > 0:
+        caps.append((omp, f"OMP_NUM_THREADS={omp}: the box's CPU share for this job"))
+    budget = CPU_RANKS_MEM_BUDGET
+    if avail:
+        budget = min(budget, avail // 2)
+    mem_cap = max(1, int(budget // max(1, per_rank_bytes)))
+    caps.append((mem_cap, f"host memory: {budget / 2**30:.0f} GiB budget / "
+                          f"{per_rank_bytes / 2**30:.2f} GiB per rank"))
+    ranks = min(c for c, _ in caps)
+    return ranks, [why for c, why in caps if c == ranks]
+
+
+def _serializer_loop(orc, spec, buf, send, recv, seconds):
+    """pack+unpack iterations, each timed, until >= 25 iterations AND >= `seconds`."""
+    times = []
+    t0 = time.perf_counter()
+    while True:
+        a = time.perf_counter()
+        orc.structured_pack(spec, buf, send)
+        orc.structured_unpack(spec, buf, recv)
+        b = time.perf_counter()
+        times.append(b - a)
+        if b - t0 >= seconds and len(times) >= 25:
+            return times, b - t0
+
+
 def cpu_baseline(N, Hw, seconds):
     """The oracle's single-thread C restatement of serialization<cpu>::pack_batch/unpack_batch
     (include/ghex/structured/pack_kernels.hpp:62-158) on the same workload, bounded in time,
-    run in a thread pinned to one core (the first core of this process's affinity set)."""
+    run in a thread pinned to one core (the first core of this process's affinity set).
+    value = throughput over the whole sample; median_of_25 = BASELINE.md §4's figure."""
     import threading
 
     import numpy as np
@@ -1479,43 +1714,42 @@ def cpu_baseline(N, Hw, seconds):
         buf = np.zeros(nbytes, np.uint8)
         orc.structured_pack(spec, buf, send)
         orc.structured_unpack(spec, buf, recv)
-        t0 = time.perf_counter()
-        it = 0
-        while True:
-            orc.structured_pack(spec, buf, send)
-            orc.structured_unpack(spec, buf, recv)
-            it += 1
-            dt = time.perf_counter() - t0
-            if dt >= seconds and it >= 3:
-                break
-        res["it"], res["dt"] = it, dt
+        res["times"], res["dt"] = _serializer_loop(orc, spec, buf, send, recv, seconds)
     th = threading.Thread(target=one)
     th.start()
     th.join()
-    it, dt = res["it"], res["dt"]
-    gbs = 4 * nbytes * it / dt / 1e9
-    out = {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-           "cpu_model": model, "nproc": nproc, "affinity_cores": len(share),
+    times, dt = res["times"], res["dt"]
+    it = len(times)
+    med = _median_of_25(times)
+    out = {"value": round(4 * nbytes * it / dt / 1e9, 3), "unit": "GB/s", "cores": 1,
+           "kind": "port", "cpu_model": model, "nproc": nproc, "affinity_cores": len(share),
            "pinned_core": share[0] if res["pinned"] else None,
+           "median_of_25_ms": round(med * 1e3, 3),
+           "median_of_25_GBps": round(4 * nbytes / med / 1e9, 3),
            "sample": f"{N}^3 fp64 H={Hw} one periodic domain, pack+unpack x{it} "
                      f"({dt:.1f} s, 1 thread pinned to core {share[0]}, "
-                     f"oracle/ghex_oracle.c row-memcpy restatement)"}
+                     f"oracle/ghex_oracle.c row-memcpy restatement); value = throughput over "
+                     f"the sample, median_of_25 = BASELINE.md §4 (25 iterations, first 5 "
+                     f"dropped, median)"}
     out["ranks"] = cpu_baseline_ranks(N, Hw, seconds, orc, nbytes, send, recv)
     return out
 
 
 def cpu_baseline_ranks(N, Hw, seconds, orc, nbytes, send, recv):
-    """the same single-threaded serializer run as independent ranks, one per host
-    core of the box's CPU share (each rank its own 512^3 domain and buffer, like the reference's
-    one-rank-per-core CPU runs), each pinned to its own core. The C oracle releases the GIL
-    inside its ctypes calls, so the ranks are threads of this process (no re-exec from a process
-    that has touched the GPU); value = bytes summed over ranks / the slowest rank's time."""
+    """SURVEY §8(d) / BASELINE.md §4: the same single-threaded serializer run as independent
+    ranks, one per core (cpu_rank_count: the affinity set, capped by the CPU quota, the box's
+    CPU share and host memory, the binding caps named in the line), each rank its own 512^3
+    domain and buffer, pinned to its own core. The C oracle releases the GIL inside its ctypes
+    calls, so the ranks are threads of this process (no re-exec from a process that has touched
+    the GPU). value = bytes summed over ranks / the slowest rank's time; median_of_25 = ranks x
+    bytes / the slowest rank's median iteration."""
     import threading
 
     import numpy as np
     model, nproc, share = _cpu_info()
-    ranks = max(1, min(16, len(share)))  # the GPU box grants 16 cores per GPU (nproc shows more)
     E = N + 2 * Hw
+    ranks, why = cpu_rank_count(share, E ** 3 * 8 + nbytes, quota=_cpu_quota(),
+                                avail=_mem_available())
     res = [None] * ranks
     pinned = [False] * ranks
     barrier = threading.Barrier(ranks)
@@ -1529,32 +1763,28 @@ def cpu_baseline_ranks(N, Hw, seconds, orc, nbytes, send, recv):
         orc.structured_pack(spec, buf, send)
         orc.structured_unpack(spec, buf, recv)
         barrier.wait()
-        t0 = time.perf_counter()
-        it = 0
-        while True:
-            orc.structured_pack(spec, buf, send)
-            orc.structured_unpack(spec, buf, recv)
-            it += 1
-            dt = time.perf_counter() - t0
-            if dt >= seconds and it >= 3:
-                break
-        res[r] = (it, dt)
+        res[r] = _serializer_loop(orc, spec, buf, send, recv, seconds)
+        del a, buf
 
     th = [threading.Thread(target=rank_fn, args=(r,)) for r in range(ranks)]
     for t in th:
         t.start()
     for t in th:
         t.join()
-    total = sum(4 * nbytes * it for it, _ in res)
+    total = sum(4 * nbytes * len(tm) for tm, _ in res)
     slowest = max(dt for _, dt in res)
-    its = [it for it, _ in res]
+    its = [len(tm) for tm, _ in res]
+    med = max(_median_of_25(tm) for tm, _ in res)
     return {"value": round(total / slowest / 1e9, 3), "unit": "GB/s", "cores": ranks,
             "kind": "port", "cpu_model": model, "nproc": nproc, "affinity_cores": len(share),
+            "cpu_quota_cores": _cpu_quota(), "rank_cap": why,
             "pinned": all(pinned),
+            "median_of_25_GBps": round(ranks * 4 * nbytes / med / 1e9, 3),
             "sample": f"{ranks} independent ranks, each a {N}^3 fp64 H={Hw} periodic domain "
                       f"pinned to its own core ({share[0]}..{share[ranks - 1]}), pack+unpack "
                       f"x{min(its)}-{max(its)} in {slowest:.1f} s, one thread each "
-                      f"(oracle/ghex_oracle.c)"}
+                      f"(oracle/ghex_oracle.c); median_of_25 = BASELINE.md §4 per rank, the "
+                      f"slowest rank's median"}
 
 
 if __name__ == "__main__":

@@ -45,12 +45,22 @@ def test_bench_line_n1_small():
     assert r["launch_us"] <= r["step_device_us"]
     assert d["fused_self"]["bytes_moved"] == 3 * (68 ** 3 - 64 ** 3) * 8
     assert "extras_error" not in d, d.get("extras_error")
+    # `verified` is the timed graph (k_copy pack + unpack) replayed on reset halos and buffers;
+    # the fused first exchange is reported separately
+    assert d["verified_fused"] is True and "timed hipGraph" in d["verified_what"]
+    for h, x in d["halo_widths"].items():
+        assert x["verified"] is True and x["verified_fused"] is True, h
+    c = r["cold_clean_kernel_events_us"]
+    assert c["pack"] > 0 and c["unpack"] > 0 and c["step_pack"] > 0 and c["step_unpack"] > 0
 
 
 def test_bench_spawns_two_ranks_rehearsal():
     d = _bench("--gpus", "2", "--rehearse", "--N", "64", "--steps", "10", "--warmup", "2",
                "--no-cold", timeout=240)
-    assert d["n_gpus"] == 2 and d["verified"] is True
+    assert d["n_gpus"] == 2 and d["verified"] is True and d["verified_fused"] is True
+    assert "transport + unpack" in d["verified_what"]
+    for h, x in d["halo_widths"].items():
+        assert x["verified"] is True, h
     assert d["config"]["decomposition"] == [2, 1, 1] and d["config"]["world_size"] == 2
     assert d["exchange_pipelined"]["verified"] is True
     assert d["unstructured_exchange"].get("verified") is True, d["unstructured_exchange"]

@@ -166,3 +166,46 @@ def test_config4_five_fields_matches_manifest(name):
     assert [f"{orc.fnv1a64(b.cpu().numpy()):016x}" for b in bases] == exp["fields"]
     del bases
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("name", [n for n in sorted(MANIFEST["full"]) if n.endswith("_P111")])
+def test_full_single_domain_two_launch_matches_manifest(name):
+    """The headline's own kernels at the headline size: the single-domain
+    512^3 plan run as the bench times it — ONE k_copy pack launch (ghx_exchange_pack), then ONE
+    k_copy unpack launch (ghx_exchange_unpack), not the fused k_self of exchange() — on a field
+    whose halos are -1 and a buffer preset to 0xFF. The packed message and the whole field after
+    the unpack must hash as the oracle's (reference path replaced:
+    include/ghex/structured/pack_kernels.hpp:161-248)."""
+    import torch
+    from ghex_amd.structured import regular as R
+    from tests.gpu_util import FakeContext
+    N, Hw, layout, parts, _ = _parse(name)
+    ranks, gf, gl = H.cube_domains(N, parts)
+    table = {0: [(d.id, d.first, d.last) for d in ranks[0]]}
+    ctx = FakeContext(0, 1, table)
+    dd = R.DomainDescriptor(ranks[0][0].id, ranks[0][0].first, ranks[0][0].last)
+    pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (1, 1, 1)), [dd])
+    base, logical = _device_linear_field(ranks[0][0], N, Hw, gl)
+    fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)
+    co = R.make_communication_object(ctx)
+    bis = [pc(fd)]
+    plan = co.plan(bis)
+    send, recv = co.buffers(plan, base.device)
+    for t in send + recv:
+        t.fill_(255)
+    co.pack_only(bis)
+    torch.cuda.synchronize()
+    exp = MANIFEST["full"][name]
+    (x,) = plan.send
+    b = send[0][:x["size"]].cpu().numpy()
+    assert {f"0:{x['pair'][0]},{x['pair'][1]}": [int(x["size"]), f"{orc.fnv1a64(b):016x}"]} \
+        == exp["messages"]
+    # the pack read only interior cells: the halos are still -1 here
+    E = N + 2 * Hw
+    assert bool((base[:Hw] == -1).all()) and bool((base[:, :, E - Hw:] == -1).all())
+    del b
+    co.unpack_only(bis)
+    torch.cuda.synchronize()
+    assert [f"{orc.fnv1a64(base.cpu().numpy()):016x}"] == exp["fields"]
+    del base, logical, send, recv
+    torch.cuda.empty_cache()
