@@ -48,6 +48,74 @@ def hostname() -> str:
     return os.environ.get("GHX_HOSTNAME") or socket.gethostname()
 
 
+def node_local_group(hosts, me):
+    """The epochs' node-local group of rank `me`: (ranks on its host in ascending order, its
+    index among them). hosts: every rank's host name, by global rank. Flag blocks are per host
+    and indexed by this position, so their size follows the ranks per host, not the world size
+    (ghx_epochs_create takes at most 64 ranks per host, any number of hosts)."""
+    local = [r for r, h in enumerate(hosts) if h == hosts[me]]
+    return local, local.index(me)
+
+
+def attach_epochs(context, hosts, timeout, sources, targets, prefix="ep"):
+    """Create (the host's lowest rank) or attach (the others) this host's flag block and set the
+    peers. Collective over the context: every rank calls it, including ranks that end up with
+    no block. sources / targets: global ranks, all on this host. Returns the ghx_epochs handle,
+    or None when this host holds only this rank."""
+    me = context.rank()
+    local, idx = node_local_group(hosts, me)
+    lead = local[0] == me
+    name = f"/ghx_{prefix}_{os.getpid()}_{secrets.token_hex(6)}" if lead and len(local) > 1 else None
+    h = None
+    if name is not None:  # created (and sized) before anyone learns its name
+        h = ctypes.c_void_p()
+        _ghx.call("ghx_epochs_create", name.encode(), 1, len(local), idx, float(timeout),
+                  ctypes.byref(h))
+    names = context.all_gather_object(name)
+    try:
+        if len(local) > 1 and not lead:
+            h = ctypes.c_void_p()
+            _ghx.call("ghx_epochs_create", names[local[0]].encode(), 0, len(local), idx,
+                      float(timeout), ctypes.byref(h))
+    finally:
+        context.all_gather_object(None)  # every rank of every host has attached (or failed)
+        if name is not None:
+            _ghx.call("ghx_epochs_unlink", name.encode())
+    if h is None:
+        return None
+    pos = {r: i for i, r in enumerate(local)}
+    for r in list(sources) + list(targets):
+        if r not in pos:
+            raise RuntimeError(f"epochs: rank {r} is not on this host ({hosts[me]!r})")
+    srcs = [pos[r] for r in sorted(set(sources))]
+    tgts = [pos[r] for r in sorted(set(targets))]
+    _ghx.call("ghx_epochs_peers", h, _ghx.i32_array(srcs), len(srcs), _ghx.i32_array(tgts),
+              len(tgts))
+    return h
+
+
+def epochs_error(ep, hosts=None, me=None):
+    """None, or a description of the epochs' recorded failure (ghx_epochs_status codes)."""
+    err = ctypes.c_int32()
+    _ghx.call("ghx_epochs_status", ep, ctypes.byref(err), None)
+    v = err.value
+    if not v:
+        return None
+    if v == 1:
+        return "a wait of the open phase timed out (a target never opened its memory)"
+    if v == 2:
+        return "a wait of the close phase timed out (a source never completed its writes)"
+    if v == 3:
+        return "the close kernel did not reach every XCD in time (fence placement)"
+    if v & 0xff == 4:
+        s = v >> 8
+        who = f"node-local rank {s}"
+        if hosts is not None and me is not None:
+            who = f"rank {node_local_group(hosts, me)[0][s]}"
+        return f"{who} failed its own open phase: its writes may have overlapped this rank's reads"
+    return f"epoch error code {v}"
+
+
 class BulkHandle:
     """Handle of a bulk exchange: wait() blocks until this rank's halos are written (and raises
     if a peer never reached the exchange); is_ready() polls."""
@@ -100,7 +168,8 @@ class BulkCommunicationObject:
         self._puts = []       # [(handle, src_ptr_array, n_src, dst_ptr_array, n_dst)]
         self._imports = []    # IPC bases to close
         self._keep = []
-        self._ep = None       # ghx_epochs handle (epochs="device", more than one rank)
+        self._ep = None       # ghx_epochs handle (epochs="device", node-local peers)
+        self._hosts = None    # every rank's host (the epochs' node-local groups)
 
     # -- setup -------------------------------------------------------------------------------
     def add_field(self, bi):
@@ -159,27 +228,17 @@ class BulkCommunicationObject:
             self._remote_bis = [part[id(bi.pattern_container)](bi.field) for bi in self._bis]
             self._co = CommunicationObject(self.context, **self.remote_options)
         if self.epochs == "device" and world > 1:
-            # one node-shared flag block per host: created by the host's lowest rank, attached by
-            # the others after an all-gather of the names, unlinked once all have attached
-            leader = local[0]
-            name = f"/ghx_ep_{os.getpid()}_{secrets.token_hex(6)}" if me == leader else None
-            if me == leader:
-                self._ep = self._epochs_attach(name, True, world, me)
-            names = self.context.all_gather_object(name)
-            if me != leader:
-                self._ep = self._epochs_attach(names[leader], False, world, me)
-            self.context.all_gather_object(None)  # every rank has attached
-            if me == leader:
-                _ghx.call("ghx_epochs_unlink", name.encode())
-            # sources: node-local ranks whose puts land in my halos; targets: those mine land in
+            # one node-shared flag block per host (created by the host's lowest rank, attached
+            # by the others, indexed by node-local position); sources: node-local ranks whose
+            # puts land in my halos; targets: those mine land in
             srcs = sorted({rr for bi in self._bis
                            for _, rr, _, _ in bi.pattern_container.recv_halos(bi.local_index)
                            if rr != me and rr in local})
             tgts = sorted({rr for bi in self._bis
                            for _, rr, _, _ in bi.pattern_container.send_halos(bi.local_index)
                            if rr != me and rr in local})
-            _ghx.call("ghx_epochs_peers", self._ep, _ghx.i32_array(srcs), len(srcs),
-                      _ghx.i32_array(tgts), len(tgts))
+            self._hosts = [info["host"] for info in allr]
+            self._ep = attach_epochs(self.context, self._hosts, self.timeout, srcs, tgts)
             self._ep_peers = (srcs, tgts)
         # target field table: (rank, domain, j) -> (rank, index in that rank's field list)
         target = {}
@@ -259,23 +318,14 @@ class BulkCommunicationObject:
         self._keep.append(keep)
         self._puts.append((h, sp, len(srcs), dp, len(dsts)))
 
-    def _epochs_attach(self, name, create, world, rank):
-        h = ctypes.c_void_p()
-        _ghx.call("ghx_epochs_create", name.encode(), 1 if create else 0, world, rank,
-                  self.timeout, ctypes.byref(h))
-        return h
-
     def check_epochs(self):
-        """Raise if a wait of this rank's epochs timed out (a peer never reached the exchange)."""
+        """Raise if this rank's epochs recorded a failure (a wait timed out: a peer never reached
+        the exchange; or a source failed its own open phase)."""
         if self._ep is None:
             return
-        err = ctypes.c_int32()
-        _ghx.call("ghx_epochs_status", self._ep, ctypes.byref(err), None)
-        if err.value:
-            phase = "open (a target never opened its halos)" if err.value == 1 else \
-                "close (a source never completed its puts)"
-            raise RuntimeError(f"bulk exchange: an epoch wait timed out after {self.timeout:.0f} s "
-                               f"in the {phase} phase")
+        why = epochs_error(self._ep, self._hosts, self.context.rank())
+        if why:
+            raise RuntimeError(f"bulk exchange failed (epoch timeout {self.timeout:.0f} s): {why}")
 
     # -- exchange ----------------------------------------------------------------------------
     def _barrier(self):

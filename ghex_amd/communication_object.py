@@ -183,9 +183,11 @@ class CommunicationHandle:
             self.wait()
             return True
         if self._event is None or self._event.query():
-            if self._co is not None:
-                self._co._valid = False
-                self._co = None
+            co, self._co = self._co, None
+            if co is not None:
+                co._valid = False
+                if co.direct:
+                    co.check_epochs()  # a poller learns of an epoch failure as wait() would
             return True
         return False
 
@@ -659,9 +661,18 @@ class CommunicationObject:
         d = self._direct.get(id(plan))
         if d is not None:
             return d
+        import torch
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("direct exchange: a plan's first exchange sets up IPC handles and "
+                               "flag blocks collectively and cannot run inside a stream capture; "
+                               "run one exchange of these fields before capturing")
         from .bulk_communication_object import hostname
         me, world = self.context.rank(), self.context.size()
         host = hostname()
+        by_peer = {}
+        for i, x in enumerate(plan.send):
+            if x["rank"] != me:
+                by_peer.setdefault(x["rank"], []).append(i)
         mine = []
         for j, x in enumerate(plan.recv):
             if x["rank"] == me:
@@ -670,19 +681,20 @@ class CommunicationObject:
             off = ctypes.c_uint64()
             _ghx.call("ghx_ipc_export", ctypes.c_void_p(recv[j].data_ptr()), h, ctypes.byref(off))
             mine.append((x["rank"], x["tag"], x["size"], bytes(h), off.value))
-        allr = self.context.all_gather_object({"host": host, "recv": mine})
+        allr = self.context.all_gather_object({"host": host, "recv": mine,
+                                               "targets": sorted(by_peer)})
+        # every rank checks every pair, so all raise together (none is left in a collective)
+        far = [(r, p) for r, a in enumerate(allr) for p in a["targets"]
+               if allr[p]["host"] != a["host"]]
+        if far:
+            r, p = far[0]
+            raise RuntimeError(f"direct exchange needs node-local peers: rank {r} (host "
+                               f"{allr[r]['host']!r}) sends to rank {p} (host "
+                               f"{allr[p]['host']!r}); use the buffered exchange across hosts")
         ptrs = [t.data_ptr() for t in send]
         imports = []
         d = {"sptrs": None, "ep": None, "imports": imports}
         self._direct[id(plan)] = d  # before anything can raise: __del__ closes what was opened
-        by_peer = {}
-        for i, x in enumerate(plan.send):
-            if x["rank"] != me:
-                by_peer.setdefault(x["rank"], []).append(i)
-        for p in by_peer:
-            if allr[p]["host"] != host:
-                raise RuntimeError(f"direct exchange: rank {p} is on host {allr[p]['host']!r}, "
-                                   f"not {host!r} (node-local peers only)")
         for i, (_, tag, size, hb, off) in direct_matches(me, plan.send,
                                                          {r: a["recv"] for r, a in enumerate(allr)}):
             base, ptr = ctypes.c_void_p(), ctypes.c_void_p()
@@ -691,28 +703,14 @@ class CommunicationObject:
             imports.append(base.value)
             ptrs[i] = ptr.value
         if world > 1:
-            # one node-shared flag block per plan: the lowest rank creates it, the others attach
-            # after an all-gather of the name, the creator unlinks it once all have attached
-            import os
-            import secrets
-            name = f"/ghx_dx_{os.getpid()}_{secrets.token_hex(6)}" if me == 0 else None
-            h = ctypes.c_void_p()
-            if me == 0:  # created (and sized) before anyone learns its name
-                _ghx.call("ghx_epochs_create", name.encode(), 1, world, me, self.epoch_timeout,
-                          ctypes.byref(h))
-                d["ep"] = h
-            names = self.context.all_gather_object(name)
-            if me != 0:
-                _ghx.call("ghx_epochs_create", names[0].encode(), 0, world, me,
-                          self.epoch_timeout, ctypes.byref(h))
-                d["ep"] = h
-            self.context.all_gather_object(None)  # every rank has attached
-            if me == 0:
-                _ghx.call("ghx_epochs_unlink", name.encode())
+            # one node-shared flag block per plan and host: the host's lowest rank creates it,
+            # the host's other ranks attach (node-local indices); ranks of other hosts take part
+            # in the collective setup only
+            from .bulk_communication_object import attach_epochs
+            d["hosts"] = [a["host"] for a in allr]
             srcs = sorted({x["rank"] for x in plan.recv if x["rank"] != me})
-            tgts = sorted(by_peer)
-            _ghx.call("ghx_epochs_peers", h, _ghx.i32_array(srcs), len(srcs),
-                      _ghx.i32_array(tgts), len(tgts))
+            d["ep"] = attach_epochs(self.context, d["hosts"], self.epoch_timeout, srcs,
+                                    sorted(by_peer), prefix="dx")
         d["sptrs"] = _ghx.ptr_array(ptrs)
         return d
 
@@ -733,16 +731,16 @@ class CommunicationObject:
         return CommunicationHandle(self, stream, self._done_event(stream))
 
     def check_epochs(self):
-        """Raise if a direct exchange's epoch wait timed out (a peer never reached it)."""
+        """Raise if a direct exchange's epochs recorded a failure (a wait timed out: a peer
+        never reached it; or a source failed its own open phase)."""
+        from .bulk_communication_object import epochs_error
         for d in self._direct.values():
             if d["ep"] is None:
                 continue
-            err = ctypes.c_int32()
-            _ghx.call("ghx_epochs_status", d["ep"], ctypes.byref(err), None)
-            if err.value:
-                raise RuntimeError(f"direct exchange: an epoch wait timed out after "
-                                   f"{self.epoch_timeout:.0f} s in the "
-                                   f"{'open' if err.value == 1 else 'close'} phase")
+            why = epochs_error(d["ep"], d.get("hosts"), self.context.rank())
+            if why:
+                raise RuntimeError(f"direct exchange failed (epoch timeout "
+                                   f"{self.epoch_timeout:.0f} s): {why}")
 
     def __del__(self):
         try:

@@ -64,8 +64,8 @@ hsa_status_t find_agents(hsa_agent_t a, void* data)
     return HSA_STATUS_SUCCESS;
 }
 
-// One wave per workgroup, enough workgroups to reach every XCD (blocks are dealt round-robin
-// over the 8 XCDs): a system-scope acquire invalidates the XCD's L2, so kernels queued after it
+// One wave per workgroup, 32 workgroups per XCD of the queried count (blocks are dealt
+// round-robin over the XCDs): a system-scope acquire invalidates the XCD's L2, so kernels queued after it
 // cannot hit lines that a copy engine has replaced behind the caches' back (copies issued
 // through HSA are invisible to the HIP runtime, which would otherwise add this acquire itself).
 __global__ __launch_bounds__(64) void k_acquire()
@@ -97,6 +97,7 @@ struct ghx_copier
     double timeout_s = 30.0;
     bool inited = false;
     int nsig = 0;
+    int acquire_groups = 256;      // k_acquire grid: 32 per XCD
 
     ~ghx_copier()
     {
@@ -203,6 +204,12 @@ int ghx_copier_create(uint64_t probe_bytes, double timeout_s, ghx_copier** out)
             hipDeviceGetAttribute(&devno, hipDeviceAttributePciDeviceId, dev) != hipSuccess ||
             hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dev) != hipSuccess)
             throw hip_error("hipDeviceGetAttribute(PCI location)");
+        // the acquire kernel must reach every XCD (each has its own L2): 32 one-wave workgroups
+        // per XCD of the queried count (blocks are dealt round-robin over the XCDs)
+        int xcc = 0;
+        if (hipDeviceGetAttribute(&xcc, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || xcc < 1)
+            throw hip_error("hipDeviceGetAttribute(number of XCCs)");
+        c->acquire_groups = 32 * xcc;
         hsa_check(hsa_init(), "hsa_init");
         c->inited = true;
         c->ag.bdf = uint32_t(bus) << 8 | uint32_t(devno) << 3;
@@ -327,7 +334,7 @@ int ghx_copier_acquire(const ghx_copier* c, ghx_stream stream)
 {
     return guarded([&] {
         if (!c) throw invalid("null copier");
-        hipLaunchKernelGGL(k_acquire, dim3(256), dim3(64), 0, static_cast<hipStream_t>(stream));
+        hipLaunchKernelGGL(k_acquire, dim3(c->acquire_groups), dim3(64), 0, static_cast<hipStream_t>(stream));
         if (hipGetLastError() != hipSuccess) throw hip_error("k_acquire launch");
         return GHX_OK;
     });

@@ -1,26 +1,41 @@
-// ghx_epochs.hip — device-side access epochs for the zero-copy (bulk) exchange: the reference's
-// access guards (include/ghex/rma/access_guard.hpp:35-140, shmem/access_guard.hpp) made
-// stream-ordered, so that an exchange is  k_epoch(open) -> puts -> k_epoch(close)  on the caller's
-// stream, with no host drain and no global barrier (include/ghex/bulk_communication_object.hpp
-// :621-694 opens every target range, puts into each source range as soon as it is writable, and
-// waits for its own target ranges to be written).
+// ghx_epochs.hip — device-side access epochs for the zero-copy exchanges (bulk puts, direct
+// pack): the reference's access guards (include/ghex/rma/access_guard.hpp:35-140,
+// shmem/access_guard.hpp) made stream-ordered, so that an exchange is
+//     k_epoch_open  ->  data launch(es)  ->  k_epoch_close
+// on the caller's stream: two small launches per exchange, no host drain, no global barrier
+// (include/ghex/bulk_communication_object.hpp:621-694 opens every target range, puts into each
+// source range as soon as it is writable, and waits for its own target ranges to be written).
 //
-// Flag block: one POSIX shared-memory segment per node-local group of ranks, registered with the
-// GPU (hipHostRegister, mapped: fine-grained, coherent host memory), so every rank's GPU reads
-// and writes every rank's flags over the same physical pages. One flag per 64-B line:
-//   epoch[r]    rank r's exchange counter (written by r only)
-//   error[r]    set by r's kernels when a wait timed out (1: open phase, 2: close phase)
-//   open[r][t]  = e: target t has opened its halos for r's puts of epoch e   (written by t)
-//   done[r][s]  = e: source s's puts of epoch e into r's halos are complete (written by s)
-// Exchange on rank R, epoch e = epoch[R] + 1:
-//   open  (before the puts): epoch[R] = e; open[s][R] = e for every source s of R; then wait
-//         until open[R][t] >= e for every target t of R (its halos are writable).
-//   close (after the puts):  system-scope release; done[t][R] = e for every target t; then wait
-//         until done[R][s] >= e for every source s (R's halos are written).
+// Flag block: one POSIX shared-memory segment per node-local group of ranks (indexed by the rank's
+// position in that group, not its global rank), registered with the GPU (hipHostRegister, mapped:
+// fine-grained, coherent host memory), so every rank's GPU reads and writes every rank's flags
+// over the same physical pages. One flag per 64-B line:
+//   epoch[r]    rank r's exchange counter (written by r only; the host reads it)
+//   error[r]    0, or why r's exchange failed (error codes below; written by r or by its peers)
+//   open[r][t]  = e: target t has opened its halos / receive buffers for r's writes of epoch e
+//   done[r][s]  = e: source s's writes of epoch e into r's memory are complete and visible
+// Device words (this rank's own GPU memory, one per 64-B line): the epoch in flight and whether
+// its open phase failed, one "written back" word per XCD and the leader's "go" word.
+//
+// Exchange on rank R, epoch e = epoch + 1:
+//   open  (one wave): epoch = e; open[s][R] = e for every source s; wait until open[R][t] >= e
+//         for every target t (their memory is writable).
+//   close (a few one-wave workgroups on EVERY XCD — the XCD count is queried, and the leader
+//         checks that each XCD really ran one):
+//         every workgroup: system-scope release (writes back its XCD's L2: the data launch's
+//           remote writes leave every XCD's L2 for the target's memory) -> "XCD x written back";
+//         leader: once every XCD has written back, done[t][R] = e for every target (with the
+//           FAIL bit when R's own open wait failed), then wait until done[R][s] >= e for every
+//           source -> "go";
+//         every workgroup, after "go": system-scope acquire (invalidates its XCD's L2 and its
+//           CU's L1), so the kernels after the close read what the sources wrote, not stale lines.
 // Every rank runs the same number of exchanges, so the epochs agree without any reset; the
-// counter lives in memory, so a captured graph replays correctly. Waits are bounded: past the
-// timeout a wave records error[R] and leaves (the host reports it), so a dead peer can never
-// hang the device.
+// counters live in memory, so a captured graph replays correctly (every replay a new epoch).
+// Waits are bounded: past the timeout a wave records error[R] and leaves, and the host raises
+// (ghx_epochs_status). A failure reaches both sides: a rank whose open wait timed out (its data
+// launch may have written into a target still reading that memory) marks its done flags FAIL,
+// and every target that sees FAIL records error 4 with the source's index; a wait also ends as
+// soon as someone has recorded an error for this rank.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
@@ -39,24 +54,35 @@ namespace ghx
 {
 namespace
 {
-constexpr int kMaxPeers = 64;
+constexpr int kMaxPeers = 63;  // lane 63 of a waiting wave polls the error line
+constexpr int kMaxXcc = 16;    // XCC_ID is a 4-bit field
+constexpr int kFencePerXcc = 4;
 constexpr uint64_t kMagic = 0x67687865706f6368ull;  // "ghxepoch"
+constexpr uint64_t kFail = 1ull << 63;              // done flag of a source whose open failed
+// error codes (error[r]; the host decodes them in ghx_epochs_status)
+constexpr uint64_t kErrOpen = 1, kErrClose = 2, kErrFence = 3, kErrPeer = 4;  // peer: 4 | s << 8
 
 struct epoch_args
 {
-    uint64_t* flags;  // device view of the flag block (8 uint64 per line)
+    uint64_t* flags;  // device view of the host flag block (8 uint64 per line)
+    uint64_t* dev;    // this rank's device words (8 uint64 per line)
     int32_t rank, world;
     int32_t n_src, n_tgt;
+    int32_t n_xcc;
     uint64_t timeout_ticks;  // wall-clock ticks (hipDeviceAttributeWallClockRate kHz)
     int16_t src[kMaxPeers], tgt[kMaxPeers];
 };
 
-// line indices inside the block
+// host block: line indices
 __host__ __device__ inline size_t l_epoch(int r, int W) { return 1 + size_t(r) * (2 + 2 * size_t(W)); }
 __host__ __device__ inline size_t l_error(int r, int W) { return l_epoch(r, W) + 1; }
 __host__ __device__ inline size_t l_open(int r, int t, int W) { return l_epoch(r, W) + 2 + size_t(t); }
 __host__ __device__ inline size_t l_done(int r, int s, int W) { return l_epoch(r, W) + 2 + size_t(W) + size_t(s); }
 inline size_t block_lines(int W) { return 1 + size_t(W) * (2 + 2 * size_t(W)); }
+// device words: line 0 = {epoch in flight, failed epoch}, 1 + x = XCD x written back, go
+constexpr size_t d_rel(int x) { return 1 + size_t(x); }
+constexpr size_t d_go = 1 + kMaxXcc;
+constexpr size_t kDevLines = d_go + 1;
 
 __device__ __forceinline__ uint64_t* at(uint64_t* f, size_t line) { return f + line * 8; }
 
@@ -64,65 +90,142 @@ __device__ __forceinline__ uint64_t sys_load(uint64_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-
+// Flag store at system scope (sc0 sc1), relaxed: no flag of this protocol publishes data
+// written by the storing wave itself. The open flags follow only reads (the stream's earlier
+// kernels are done with the memory: kernel-boundary order); the done flags follow the per-XCD
+// release of every workgroup of the close kernel, which the leader has observed before it
+// stores them (each "XCD written back" word is stored after that XCD's buffer_wbl2 and an
+// explicit wait for it).
 __device__ __forceinline__ void sys_store(uint64_t* p, uint64_t v)
 {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t dev_load(uint64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void dev_store(uint64_t* p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave. phase 0 = open, 1 = close. Lane i signals peer i of one list and waits on peer i of
-// the other; every flag address is per lane (vector memory operations only).
-__global__ __launch_bounds__(64) void k_epoch(epoch_args a, int phase)
+__device__ __forceinline__ unsigned xcc_id()
+{
+    // HW_REG_XCC_ID (hwreg 20), bits 3:0: the XCD this wave runs on (gfx940+)
+    return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf;
+}
+
+// One wave: every lane with a flag polls it until it reaches e (flag values may carry kFail);
+// lane 63 polls R's error line. Returns 0 once every flag has arrived, the recorded error as
+// soon as one is set (by R's own earlier wave or by a peer), or `code` after recording it on
+// timeout. *seen: the lane's last flag value (for the FAIL bit).
+__device__ uint64_t wave_wait(uint64_t* err_line, uint64_t* flag, uint64_t e, uint64_t timeout,
+                              uint64_t code, uint64_t* seen)
+{
+    const int lane = int(threadIdx.x);
+    uint64_t* p = lane == 63 ? err_line : flag;
+    const uint64_t t0 = wall_clock64();
+    for (;;)
+    {
+        const uint64_t v = p ? sys_load(p) : 0;
+        const uint64_t err = __shfl(v, 63);
+        if (err) return err;
+        *seen = v;
+        const bool pending = lane != 63 && flag && (v & ~kFail) < e;
+        if (!__any(pending)) return 0;
+        if (wall_clock64() - t0 > timeout)
+        {
+            if (lane == 63) sys_store(err_line, code);
+            return code;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+// One wave: lanes with a device word poll it until it reaches e. False on timeout.
+__device__ bool wave_wait_dev(uint64_t* word, uint64_t e, uint64_t timeout)
+{
+    const uint64_t t0 = wall_clock64();
+    for (;;)
+    {
+        const uint64_t v = word ? dev_load(word) : e;
+        if (!__any(v < e)) return true;
+        if (wall_clock64() - t0 > timeout) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_epoch_open(epoch_args a)
 {
     const int lane = int(threadIdx.x);
     const int R = a.rank, W = a.world;
     uint64_t* f = a.flags;
-    uint64_t e = sys_load(at(f, l_epoch(R, W)));
-    if (phase == 0)
+    const uint64_t e = dev_load(at(a.dev, 0)) + 1;
+    if (lane == 0)
     {
-        e += 1;
-        if (lane == 0) sys_store(at(f, l_epoch(R, W)), e);
-        if (lane < a.n_src) sys_store(at(f, l_open(a.src[lane], R, W)), e);  // halos open
+        dev_store(at(a.dev, 0), e);
+        sys_store(at(f, l_epoch(R, W)), e);  // the host's view (ghx_epochs_status)
     }
-    else
+    if (lane < a.n_src) sys_store(at(f, l_open(a.src[lane], R, W)), e);  // halos / buffers open
+    uint64_t seen;
+    const uint64_t err = wave_wait(at(f, l_error(R, W)),
+                                   lane < a.n_tgt ? at(f, l_open(R, a.tgt[lane], W)) : nullptr, e,
+                                   a.timeout_ticks, kErrOpen, &seen);
+    // a failed open phase makes this epoch's done flags FAIL (the data launch runs anyway: its
+    // writes may have hit memory a target was still reading, and the target must know)
+    if (err && lane == 0) dev_store(at(a.dev, 0) + 1, e);
+    // no fence: nothing read after this depends on the flags (the data launch that follows only
+    // writes, and starts after this kernel has ended)
+}
+
+__global__ __launch_bounds__(64) void k_epoch_close(epoch_args a)
+{
+    const int lane = int(threadIdx.x);
+    const int R = a.rank, W = a.world;
+    uint64_t* f = a.flags;
+    uint64_t* dv = a.dev;
+    // the data launch's writes into the targets' memory leave this XCD's L2: the write-back is
+    // issued first and overlaps the loads of the epoch words; the explicit wait covers both
+    if (a.n_tgt > 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    const uint64_t e = dev_load(at(dv, 0));
+    const bool open_failed = dev_load(at(dv, 0) + 1) == e;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.n_tgt > 0 && lane == 0) dev_store(at(dv, d_rel(int(xcc_id()))), e);
+    if (blockIdx.x == 0)
     {
-        // the puts of this epoch (earlier launches on this stream) before the done flags
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-        if (lane < a.n_tgt) sys_store(at(f, l_done(a.tgt[lane], R, W)), e);
-    }
-    const int n = phase == 0 ? a.n_tgt : a.n_src;
-    if (lane < n)
-    {
-        uint64_t* p = phase == 0 ? at(f, l_open(R, a.tgt[lane], W)) : at(f, l_done(R, a.src[lane], W));
-        const uint64_t t0 = wall_clock64();
-        while (sys_load(p) < e)
+        uint64_t seen = 0;
+        uint64_t err = 0;
+        // every XCD has written back (and the grid really reached every XCD)
+        if (a.n_tgt > 0 &&
+            !wave_wait_dev(lane < a.n_xcc ? at(dv, d_rel(lane)) : nullptr, e, a.timeout_ticks))
         {
-            if (wall_clock64() - t0 > a.timeout_ticks)
-            {
-                sys_store(at(f, l_error(R, W)), uint64_t(phase + 1));
-                break;
-            }
-            __builtin_amdgcn_s_sleep(8);
+            err = kErrFence;
+            if (lane == 0) sys_store(at(f, l_error(R, W)), kErrFence);
         }
+        const uint64_t mark = (open_failed || err) ? kFail : 0;
+        if (lane < a.n_tgt) sys_store(at(f, l_done(a.tgt[lane], R, W)), e | mark);
+        if (!err)
+        {
+            err = wave_wait(at(f, l_error(R, W)),
+                            lane < a.n_src ? at(f, l_done(R, a.src[lane], W)) : nullptr, e,
+                            a.timeout_ticks, kErrClose, &seen);
+            // a source whose open failed: its writes may have overlapped this rank's last reads
+            const bool bad = !err && lane < a.n_src && lane != 63 && (seen & kFail);
+            const uint64_t m = __ballot(bad);
+            if (m && lane == int(__builtin_ctzll(m)))
+                sys_store(at(f, l_error(R, W)), kErrPeer | (uint64_t(a.src[lane]) << 8));
+        }
+        if (lane == 0 && a.n_src > 0) dev_store(at(dv, d_go), e);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-}
-// Grid-wide system-scope fences, one wave per workgroup and kFenceGroups workgroups so that
-// every XCD runs some (blocks are dealt round-robin over the 8 XCDs, each with its own L2). The
-// fences in k_epoch run on ONE XCD; a peer's puts land in the target GPU's memory over xGMI, so
-// the source writes back every XCD's L2 before signalling done (k_sys_release) and the target
-// invalidates every XCD's L2 after its wait (k_sys_acquire), before its kernels read the halos.
-constexpr int kFenceGroups = 64;
-
-__global__ __launch_bounds__(64) void k_sys_release()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __builtin_amdgcn_s_waitcnt(0);  // the write-back has completed before the wave ends
-}
-
-__global__ __launch_bounds__(64) void k_sys_acquire()
-{
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    else if (a.n_src > 0)
+    {
+        if (!wave_wait_dev(lane == 0 ? at(dv, d_go) : nullptr, e, a.timeout_ticks) && lane == 0)
+            sys_store(at(f, l_error(R, W)), kErrFence);
+    }
+    // what the sources wrote is read by the kernels after this one: no stale line in this XCD's
+    // L2 (nor this CU's L1; the next launch invalidates the other CUs' L1s). A rank without
+    // sources reads nothing new and skips it.
+    if (a.n_src > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
 }
 }  // namespace
 }  // namespace ghx
@@ -135,9 +238,12 @@ struct ghx_epochs
     void* host = nullptr;  // the mapping
     size_t bytes = 0;
     bool registered = false;
+    uint64_t* dev = nullptr;
+    int fence_groups = 0;
     epoch_args args{};
     ~ghx_epochs()
     {
+        if (dev) (void)hipFree(dev);
         if (registered) (void)hipHostUnregister(host);
         if (host) munmap(host, bytes);
     }
@@ -153,8 +259,8 @@ int ghx_epochs_create(const char* name, int32_t create, int32_t world, int32_t r
         if (!name || !out) throw invalid("null argument");
         *out = nullptr;
         if (name[0] != '/' || std::strchr(name + 1, '/')) throw invalid("shm name must be \"/name\"");
-        if (world < 1 || world > kMaxPeers || rank < 0 || rank >= world)
-            throw invalid("world must be in [1, 64] and rank in [0, world)");
+        if (world < 1 || world > kMaxPeers + 1 || rank < 0 || rank >= world)
+            throw invalid("world (the node-local group) must be in [1, 64] and rank in [0, world)");
         if (!(timeout_s > 0)) throw invalid("timeout must be > 0");
         // the creating rank removes the name again if anything below fails (no stale segment)
         struct unlink_on_fail
@@ -204,13 +310,24 @@ int ghx_epochs_create(const char* name, int32_t create, int32_t world, int32_t r
         void* dptr = nullptr;
         if (hipHostGetDevicePointer(&dptr, ep->host, 0) != hipSuccess)
             throw hip_error("hipHostGetDevicePointer(flag block)");
-        int dev = 0, khz = 0;
+        int dev = 0, khz = 0, xcc = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
             throw hip_error("hipDeviceGetAttribute(wall clock rate)");
+        // the close kernel's fences must run on every XCD (each has its own L2): its grid is
+        // sized from the XCD count, and its leader checks that every XCD reported
+        if (hipDeviceGetAttribute(&xcc, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || xcc < 1 ||
+            xcc > kMaxXcc)
+            throw hip_error("hipDeviceGetAttribute(number of XCCs) gave no usable count");
+        if (hipMalloc(&ep->dev, kDevLines * 64) != hipSuccess) throw hip_error("hipMalloc(epoch words)");
+        if (hipMemset(ep->dev, 0, kDevLines * 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            throw hip_error("hipMemset(epoch words)");
+        ep->fence_groups = kFencePerXcc * xcc;
         ep->args.flags = static_cast<uint64_t*>(dptr);
+        ep->args.dev = ep->dev;
         ep->args.rank = rank;
         ep->args.world = world;
+        ep->args.n_xcc = xcc;
         ep->args.timeout_ticks = uint64_t(timeout_s * 1e3 * double(khz));
         cleanup.armed = false;
         *out = ep.release();
@@ -234,12 +351,12 @@ int ghx_epochs_peers(ghx_epochs* ep, const int32_t* sources, int32_t n_sources,
         if (!ep) throw invalid("null epochs");
         if (n_sources < 0 || n_targets < 0 || n_sources > kMaxPeers || n_targets > kMaxPeers ||
             (n_sources && !sources) || (n_targets && !targets))
-            throw invalid("bad peer lists (at most 64 each)");
+            throw invalid("bad peer lists (at most 63 each)");
         for (int i = 0; i < n_sources + n_targets; ++i)
         {
             const int32_t r = i < n_sources ? sources[i] : targets[i - n_sources];
             if (r < 0 || r >= ep->args.world || r == ep->args.rank)
-                throw invalid("peer rank out of range (or this rank itself)");
+                throw invalid("peer out of range of the node-local group (or this rank itself)");
         }
         ep->args.n_src = n_sources;
         ep->args.n_tgt = n_targets;
@@ -249,26 +366,27 @@ int ghx_epochs_peers(ghx_epochs* ep, const int32_t* sources, int32_t n_sources,
     });
 }
 
-// phase 0: open (before this rank's puts), 1: close (after them; bracketed by the grid-wide
-// release / acquire when this rank has targets / sources)
+// phase 0: open (before this rank's data launch), 1: close (after it). Two launches per exchange.
 int ghx_epochs_enqueue(const ghx_epochs* ep, int32_t phase, ghx_stream stream)
 {
     return guarded([&] {
         if (!ep) throw invalid("null epochs");
         if (phase != 0 && phase != 1) throw invalid("phase must be 0 (open) or 1 (close)");
         const auto s = static_cast<hipStream_t>(stream);
-        if (phase == 1 && ep->args.n_tgt > 0)
-            hipLaunchKernelGGL(k_sys_release, dim3(kFenceGroups), dim3(64), 0, s);
-        hipLaunchKernelGGL(k_epoch, dim3(1), dim3(64), 0, s, ep->args, int(phase));
-        if (phase == 1 && ep->args.n_src > 0)
-            hipLaunchKernelGGL(k_sys_acquire, dim3(kFenceGroups), dim3(64), 0, s);
+        if (phase == 1 && ep->args.n_src == 0 && ep->args.n_tgt == 0) return GHX_OK;  // no peers
+        if (phase == 0)
+            hipLaunchKernelGGL(k_epoch_open, dim3(1), dim3(64), 0, s, ep->args);
+        else
+            hipLaunchKernelGGL(k_epoch_close, dim3(ep->fence_groups), dim3(64), 0, s, ep->args);
         if (hipGetLastError() != hipSuccess) throw hip_error("k_epoch launch");
         return GHX_OK;
     });
 }
 
-// *error: 0, or 1 / 2 when a wait of the open / close phase timed out (a peer never reached the
-// exchange); *epoch: this rank's exchange counter. Host reads of the coherent flag block.
+// *error: 0, 1 / 2 when a wait of the open / close phase timed out (a peer never reached the
+// exchange), 3 when the close kernel's workgroups did not reach every XCD in time, 4 | s << 8
+// when source s (node-local index) failed its own open phase; *epoch: this rank's exchange
+// counter. Host reads of the coherent flag block.
 int ghx_epochs_status(const ghx_epochs* ep, int32_t* error, uint64_t* epoch)
 {
     return guarded([&] {
@@ -276,6 +394,17 @@ int ghx_epochs_status(const ghx_epochs* ep, int32_t* error, uint64_t* epoch)
         const int R = ep->args.rank, W = ep->args.world;
         if (error) *error = int32_t(ep->line(l_error(R, W))[0]);
         if (epoch) *epoch = ep->line(l_epoch(R, W))[0];
+        return GHX_OK;
+    });
+}
+
+// The XCD count the close kernel was sized for and its grid.
+int ghx_epochs_info(const ghx_epochs* ep, int32_t* n_xcc, int32_t* fence_groups)
+{
+    return guarded([&] {
+        if (!ep) throw invalid("null epochs");
+        if (n_xcc) *n_xcc = ep->args.n_xcc;
+        if (fence_groups) *fence_groups = ep->fence_groups;
         return GHX_OK;
     });
 }

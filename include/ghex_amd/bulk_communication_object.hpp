@@ -60,10 +60,7 @@ class bulk_handle
         if (!m_ep) return;
         std::int32_t err = 0;
         check_ghx(ghx_epochs_status(m_ep, &err, nullptr), "ghx_epochs_status");
-        if (err)
-            throw std::runtime_error(std::string("bulk exchange: an epoch wait timed out in the ") +
-                                     (err == 1 ? "open phase (a target never opened its halos)"
-                                               : "close phase (a source never completed its puts)"));
+        if (err) throw std::runtime_error("bulk exchange failed: " + epochs_error_text(err));
     }
 
   public:
@@ -355,6 +352,11 @@ class bulk_communication_object
                 if (local[std::size_t(q)] && all[std::size_t(q)].pid == all[std::size_t(r)].pid) distinct = false;
         }
         distinct = distinct && nlocal > 1;
+        // the flag block is indexed by node-local position (its size follows the ranks per
+        // host, not the world size)
+        std::vector<std::int32_t> pos(std::size_t(world), -1);
+        for (int r = 0, k = 0; r < world; ++r)
+            if (local[std::size_t(r)]) pos[std::size_t(r)] = k++;
         // one flag block per host: its lowest rank creates it, publishes the name in a second
         // round, the others attach, the creator unlinks it once all have
         std::string name;
@@ -362,7 +364,8 @@ class bulk_communication_object
         {
             name = "/ghx_ep_" + std::to_string(getpid()) + "_" +
                    std::to_string(reinterpret_cast<std::uintptr_t>(this) & 0xffffffu);
-            check_ghx(ghx_epochs_create(name.c_str(), 1, world, me, epoch_timeout, &m_ep), "ghx_epochs_create");
+            check_ghx(ghx_epochs_create(name.c_str(), 1, nlocal, pos[std::size_t(me)], epoch_timeout, &m_ep),
+                      "ghx_epochs_create");
         }
         if (world > 1)
         {
@@ -370,8 +373,8 @@ class bulk_communication_object
             if (distinct && me != leader)
             {
                 const auto& ln = names[std::size_t(leader)];
-                check_ghx(ghx_epochs_create(std::string(ln.begin(), ln.end()).c_str(), 0, world, me, epoch_timeout,
-                                            &m_ep),
+                check_ghx(ghx_epochs_create(std::string(ln.begin(), ln.end()).c_str(), 0, nlocal,
+                                            pos[std::size_t(me)], epoch_timeout, &m_ep),
                           "ghx_epochs_create");
             }
             barrier();  // every rank attached
@@ -386,8 +389,9 @@ class bulk_communication_object
                     {
                         const int rr = std::get<1>(h);
                         auto& v = dir == 0 ? tgts : srcs;
-                        if (rr != me && local[std::size_t(rr)] && std::find(v.begin(), v.end(), rr) == v.end())
-                            v.push_back(rr);
+                        const std::int32_t lr = pos[std::size_t(rr)];  // node-local index
+                        if (rr != me && local[std::size_t(rr)] && std::find(v.begin(), v.end(), lr) == v.end())
+                            v.push_back(lr);
                     }
             std::sort(srcs.begin(), srcs.end());
             std::sort(tgts.begin(), tgts.end());

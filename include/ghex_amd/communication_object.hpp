@@ -48,6 +48,22 @@ inline void check_ghx(int rc, const char* what)
     if (rc != GHX_OK) throw std::runtime_error(std::string(what) + " failed: " + ghx_last_error());
 }
 
+// ghx_epochs_status codes as text (the zero-copy exchanges' failures)
+inline std::string epochs_error_text(std::int32_t err)
+{
+    switch (err)
+    {
+        case 1: return "a wait of the open phase timed out (a target never opened its memory)";
+        case 2: return "a wait of the close phase timed out (a source never completed its writes)";
+        case 3: return "the close kernel did not reach every XCD in time (fence placement)";
+        default: break;
+    }
+    if ((err & 0xff) == 4)
+        return "node-local rank " + std::to_string(err >> 8) +
+               " failed its own open phase: its writes may have overlapped this rank's reads";
+    return "epoch error code " + std::to_string(err);
+}
+
 // ghex::context (include/ghex/context.hpp): the process group the patterns and exchanges span.
 class context
 {
@@ -471,10 +487,7 @@ class communication_object
             if (!kv.second->ep) continue;
             std::int32_t err = 0;
             check_ghx(ghx_epochs_status(kv.second->ep, &err, nullptr), "ghx_epochs_status");
-            if (err)
-                throw std::runtime_error(std::string("direct exchange: an epoch wait timed out in the ") +
-                                         (err == 1 ? "open phase (a receiver never freed its buffers)"
-                                                   : "close phase (a sender never completed its pack)"));
+            if (err) throw std::runtime_error("direct exchange failed: " + epochs_error_text(err));
         }
     }
 
@@ -539,6 +552,14 @@ class communication_object
                 recv_of[std::size_t(r)].push_back(e);
             }
         }
+        // every rank checks every pair (the receivers' entries name their senders), so all
+        // throw together and none is left waiting in a collective
+        for (int r = 0; r < world; ++r)
+            for (const auto& e : recv_of[std::size_t(r)])
+                if (e.src >= 0 && e.src < world && hosts[std::size_t(e.src)] != hosts[std::size_t(r)])
+                    throw std::runtime_error("direct exchange needs node-local peers: rank " + std::to_string(e.src) +
+                                             " (host " + hosts[std::size_t(e.src)] + ") sends to rank " +
+                                             std::to_string(r) + " (host " + hosts[std::size_t(r)] + ")");
         p.dsptr = p.sptr;
         std::map<int, std::vector<std::size_t>> by_peer;
         for (std::size_t i = 0; i < p.send.size(); ++i)
@@ -574,29 +595,44 @@ class communication_object
         }
         if (world > 1)
         {
+            // one flag block per plan and host, indexed by node-local position: the host's
+            // lowest rank creates it, the host's other ranks attach
+            std::vector<std::int32_t> pos(std::size_t(world), -1);
+            int leader = -1, nlocal = 0;
+            for (int r = 0; r < world; ++r)
+                if (hosts[std::size_t(r)] == host)
+                {
+                    if (leader < 0) leader = r;
+                    pos[std::size_t(r)] = nlocal++;
+                }
             std::string name;
-            if (me == 0)  // created (and sized) before anyone learns its name
+            if (me == leader && nlocal > 1)  // created (and sized) before anyone learns its name
             {
                 name = "/ghx_dx_" + std::to_string(getpid()) + "_" +
                        std::to_string(reinterpret_cast<std::uintptr_t>(&p) & 0xffffffu);
-                check_ghx(ghx_epochs_create(name.c_str(), 1, world, me, m_opt.epoch_timeout, &p.ep),
+                check_ghx(ghx_epochs_create(name.c_str(), 1, nlocal, pos[std::size_t(me)], m_opt.epoch_timeout,
+                                            &p.ep),
                           "ghx_epochs_create");
             }
             const auto names = t.all_gather(std::vector<char>(name.begin(), name.end()));
-            if (me != 0)
-                check_ghx(ghx_epochs_create(std::string(names[0].begin(), names[0].end()).c_str(), 0, world, me,
-                                            m_opt.epoch_timeout, &p.ep),
+            if (me != leader && nlocal > 1)
+                check_ghx(ghx_epochs_create(std::string(names[std::size_t(leader)].begin(),
+                                                        names[std::size_t(leader)].end()).c_str(),
+                                            0, nlocal, pos[std::size_t(me)], m_opt.epoch_timeout, &p.ep),
                           "ghx_epochs_create");
             (void)t.all_gather({});  // every rank has attached
-            if (me == 0) (void)ghx_epochs_unlink(name.c_str());
+            if (me == leader && nlocal > 1) (void)ghx_epochs_unlink(name.c_str());
             std::vector<std::int32_t> srcs, tgts;
             for (auto& b : p.recv)
-                if (b.rank != me && std::find(srcs.begin(), srcs.end(), b.rank) == srcs.end()) srcs.push_back(b.rank);
-            for (auto& kv : by_peer) tgts.push_back(kv.first);
+                if (b.rank != me && std::find(srcs.begin(), srcs.end(), pos[std::size_t(b.rank)]) == srcs.end())
+                    srcs.push_back(pos[std::size_t(b.rank)]);
+            for (auto& kv : by_peer) tgts.push_back(pos[std::size_t(kv.first)]);
             std::sort(srcs.begin(), srcs.end());
-            check_ghx(ghx_epochs_peers(p.ep, srcs.data(), std::int32_t(srcs.size()), tgts.data(),
-                                       std::int32_t(tgts.size())),
-                      "ghx_epochs_peers");
+            std::sort(tgts.begin(), tgts.end());
+            if (p.ep)
+                check_ghx(ghx_epochs_peers(p.ep, srcs.data(), std::int32_t(srcs.size()), tgts.data(),
+                                           std::int32_t(tgts.size())),
+                          "ghx_epochs_peers");
         }
     }
 

@@ -429,19 +429,24 @@ int ghx_put_execute(const ghx_put* put, void* const* src_fields, int32_t n_src,
 int ghx_put_info(const ghx_put* put, uint64_t* bytes, int32_t* n_tiles);
 int ghx_put_destroy(ghx_put* put);
 
-/* Device-side access epochs of the bulk exchange: the reference's access guards
- * (include/ghex/rma/access_guard.hpp:35-140; per range: start/end_target_epoch on the owner,
- * start/end_source_epoch on the putter; include/ghex/bulk_communication_object.hpp:621-694)
- * as two stream-ordered single-wave kernels around the puts, over a flag block in node-shared
- * host memory (POSIX shm `name`, "/..."; the creating rank passes create = 1 before the others
- * attach with 0, and one rank unlinks the name once all have attached). ghx_epochs_peers sets
- * this rank's sources (ranks that put into its halos) and targets (ranks whose halos it puts
- * into), excluding itself. ghx_epochs_enqueue(phase 0) opens this rank's halos to its sources
- * and waits until each target has opened its halos; phase 1 (after the puts) signals each
- * target that the puts of this epoch are complete and waits for each source's. No host
- * synchronisation, no barrier; the epoch counter lives in the block, so the sequence can be
- * captured into a graph. A wait that exceeds `timeout_s` records an error (ghx_epochs_status:
- * 1 = open phase, 2 = close phase) instead of hanging the device. */
+/* Device-side access epochs of the zero-copy exchanges (bulk puts, direct pack): the reference's
+ * access guards (include/ghex/rma/access_guard.hpp:35-140; per range: start/end_target_epoch on
+ * the owner, start/end_source_epoch on the putter; include/ghex/bulk_communication_object.hpp
+ * :621-694) as TWO stream-ordered launches around the data launch(es) — phase 0 (open) before,
+ * phase 1 (close) after — over a flag block in node-shared host memory (POSIX shm `name`,
+ * "/..."; the creating rank passes create = 1 before the others attach with 0, and one rank
+ * unlinks the name once all have attached). `world` and `rank` are the node-local group's size
+ * and this rank's index in it (one block per host; at most 64 ranks per host). ghx_epochs_peers
+ * sets this rank's sources (ranks that write into its memory) and targets (ranks whose memory it
+ * writes into) as node-local indices, excluding itself. Open: this rank's halos / receive
+ * buffers are open to its sources; wait until each target has opened. Close: system-scope
+ * release on every XCD (the grid is sized from the queried XCD count; the leader checks that
+ * every XCD ran), signal each target, wait for each source, system-scope acquire on every XCD.
+ * No host synchronisation, no barrier; the epoch counter lives in memory, so the sequence can
+ * be captured into a graph. Waits are bounded: ghx_epochs_status reports 0, 1 / 2 (a wait of
+ * the open / close phase timed out), 3 (the close kernel did not reach every XCD in time) or
+ * 4 | s << 8 (source s failed its own open phase: its writes may have overlapped this rank's
+ * reads). After a nonzero status the object is broken (every later wait returns at once). */
 typedef struct ghx_epochs ghx_epochs;
 int ghx_epochs_create(const char* name, int32_t create, int32_t world, int32_t rank,
                       double timeout_s, ghx_epochs** out);
@@ -450,6 +455,7 @@ int ghx_epochs_peers(ghx_epochs* ep, const int32_t* sources, int32_t n_sources,
                      const int32_t* targets, int32_t n_targets);
 int ghx_epochs_enqueue(const ghx_epochs* ep, int32_t phase, ghx_stream stream);
 int ghx_epochs_status(const ghx_epochs* ep, int32_t* error, uint64_t* epoch);
+int ghx_epochs_info(const ghx_epochs* ep, int32_t* n_xcc, int32_t* fence_groups);
 int ghx_epochs_destroy(ghx_epochs* ep);
 
 /* ------------------------------------------------------------------------------------------

@@ -45,7 +45,7 @@
 #include <ghex_amd/data_descriptor.hpp>
 #include <ghex_amd/field_descriptor.hpp>
 #include <ghex_amd/rccl_transport.hpp>
-#include <ghex_amd/shm_transport.hpp>
+#include "shm_transport.hpp"  // test infrastructure: ranks as processes sharing the one test GPU
 
 #include <atomic>
 #include <chrono>

@@ -1,4 +1,5 @@
-// ghex_amd/shm_transport.hpp — ranks as separate PROCESSES of one host, meeting in a named POSIX
+// tests/cpp/shm_transport.hpp — TEST INFRASTRUCTURE, not product (transports are out of scope,
+// SURVEY §2 row 9): ranks as separate PROCESSES of one host, meeting in a named POSIX
 // shared-memory segment: the setup all_gather and a host-staged exchange (device buffer -> the
 // segment's pages -> device buffer). In the reference's terms: the MPI communicator's all_gather
 // of the setup (include/ghex/mpi/communicator.hpp:63-345) and oomph's host-buffer message path
@@ -41,7 +42,7 @@
 #include <map>
 #include <thread>
 
-#include "transport.hpp"
+#include <ghex_amd/transport.hpp>
 
 namespace ghex_amd
 {

@@ -37,6 +37,8 @@ def main():
     ghex_amd.native_library()
     if mode == "udirect":
         sys.exit(unstructured_direct(rank, world, N, Hw, reps))
+    if mode in ("slowdirect", "slowbulk"):
+        sys.exit(slow_peer(mode, rank, world, N, Hw, (px, py, pz)))
     ranks, gf, gl = H.cube_domains(N, (px, py, pz))
     dom = ranks[rank][0]
     ctx = ghex_amd.make_context()
@@ -184,6 +186,58 @@ def main():
     del co
     dist.destroy_process_group()
     sys.exit(0 if int(t.item()) == 0 else 1)
+
+
+def slow_peer(mode, rank, world, N, Hw, parts):
+    """Modes slowdirect / slowbulk (an epoch failure must reach both sides): after
+    one good exchange, rank 1 arrives 5 s late at the second one while the epoch timeout is
+    1.5 s. Rank 0's open wait times out — its data launch still writes into rank 1's memory —
+    so rank 0 must raise the open-phase timeout and rank 1, whose own waits pass, must raise that
+    rank 0 failed its open phase (the FAIL mark on rank 0's done flag). Exit 0 when both do."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+    import ghex_amd
+    from ghex_amd.structured import regular as R
+    from tests import helpers as H
+    from tests.gpu_util import device_field
+    ranks, gf, gl = H.cube_domains(N, parts)
+    dom = ranks[rank][0]
+    ctx = ghex_amd.make_context()
+    dd = R.DomainDescriptor(dom.id, dom.first, dom.last)
+    pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (True,) * 3), [dd])
+    a, _ = H.linear_index_field(dom, N, Hw, gl)
+    base, logical = device_field(a, (2, 1, 0))
+    fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)
+    if mode == "slowdirect":
+        co = R.make_communication_object(ctx, direct=True, epoch_timeout=1.5)
+        ex = lambda: co.exchange([pc(fd)])  # noqa: E731
+    else:
+        co = ghex_amd.make_bulk_communication_object(ctx, timeout=1.5)
+        co.add_field(pc(fd))
+        ex = co.exchange
+    ex().wait()  # both on time
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank == 1:
+        time.sleep(5.0)
+    err = ""
+    try:
+        ex().wait()
+    except RuntimeError as e:
+        err = str(e)
+    want = "open phase timed out" if rank == 0 else "failed its own open phase"
+    ok = want in err
+    print(f"{mode} rank {rank}: {'ok' if ok else 'WRONG'}: {err or 'no error raised'}", flush=True)
+    t = torch.tensor([0 if ok else 1])
+    dist.all_reduce(t)
+    if rank == 0 and int(t.item()) == 0:
+        print(f"{mode} world {world}: bad cells 0 (both sides raised)")
+    dist.barrier()
+    del co
+    dist.destroy_process_group()
+    return 0 if int(t.item()) == 0 else 1
 
 
 def unstructured_direct(rank, world, cells, levels, reps):

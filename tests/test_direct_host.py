@@ -37,3 +37,42 @@ def test_disagreements_raise(recv, msg):
 
 def test_no_peers_no_matches():
     assert direct_matches(3, _send((3, 1, 8), (3, 2, 8)), {}) == []
+
+
+def test_epochs_group_is_node_local_beyond_64_ranks():
+    """the epochs' flag block is per host and indexed by node-local position, so a
+    job of 9 hosts x 8 ranks (72 > the 64-rank block limit) maps every rank to [0, 8)."""
+    from ghex_amd.bulk_communication_object import node_local_group
+    hosts = [f"node{r // 8}" for r in range(72)]
+    for me in range(72):
+        local, idx = node_local_group(hosts, me)
+        assert local == list(range(8 * (me // 8), 8 * (me // 8) + 8))
+        assert idx == me % 8 and len(local) <= 64
+    # hosts interleaved by rank: positions follow ascending global rank on each host
+    hosts = [f"h{r % 3}" for r in range(10)]
+    assert node_local_group(hosts, 7) == ([1, 4, 7], 2)
+    assert node_local_group(hosts, 9) == ([0, 3, 6, 9], 3)
+
+
+def test_epoch_error_codes_decode():
+    """ghx_epochs_status codes as the Python objects report them (the host side of the device
+    epochs; the codes themselves are set by ghx_epochs.hip)."""
+    import ctypes
+    from ghex_amd import bulk_communication_object as B
+    from ghex_amd import _ghx
+    orig = _ghx.call
+
+    def fake(code):
+        def call(name, ep, err, epoch):
+            assert name == "ghx_epochs_status"
+            err._obj.value = code
+        return call
+    hosts = ["a", "b", "a", "a"]
+    try:
+        for code, text in ((0, None), (1, "open phase timed out"), (2, "close phase timed out"),
+                           (3, "every XCD"), (4 | (1 << 8), "rank 2 failed its own open")):
+            _ghx.call = fake(code)
+            got = B.epochs_error(ctypes.c_void_p(1), hosts, 0)
+            assert (got is None) if text is None else (text in got), (code, got)
+    finally:
+        _ghx.call = orig

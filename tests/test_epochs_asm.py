@@ -1,0 +1,126 @@
+"""CPU: the cross-GPU ordering of the zero-copy exchanges, pinned in the gfx950 machine code
+(VERDICT r03 next #3a). The one-GPU test box cannot exercise writes that land in another chip's
+HBM over xGMI, so what makes them safe is checked where it lives — the instructions hipcc emits
+for the epoch kernels (ghex_amd/csrc/ghx_epochs.hip) and for the kernels that write peer memory
+(k_copy: the direct exchange's pack; k_put: the bulk puts; ghex_amd/csrc/ghx_kernels.hip):
+
+* every system-scope release (`buffer_wbl2 sc0 sc1`) is followed at once by a wait for it
+  (`s_waitcnt vmcnt(0)`), so no flag store can overtake the write-back;
+* the close kernel reads the XCD id (placement is checked, not assumed), releases before it
+  publishes "this XCD is written back", and ends in a system-scope acquire (`buffer_inv sc0 sc1`)
+  behind a wait (ranks with sources; nothing touches memory after it); the open kernel, whose
+  flags follow reads only, has no fence;
+* every flag access in host memory is a system-scope vector access (`sc0 sc1`), every device
+  word an agent-scope one (`sc1`), none through `flat_` instructions;
+* the peer-writing kernels store through `global_store_*` (no `flat_`, no non-temporal stores
+  whose write-back the release would not cover).
+Reference: include/ghex/rma/cuda/handle.hpp:20-96 (the CUDA IPC path these replace)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = "/opt/rocm/bin/hipcc"
+pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not present")
+
+
+def _asm(src, tmp_path):
+    out = tmp_path / (os.path.basename(src) + ".s")
+    subprocess.run([HIPCC, "-std=c++17", "-O3", "-I" + os.path.join(ROOT, "include"),
+                    "-I" + os.path.join(ROOT, "ghex_amd", "csrc"), "--offload-arch=gfx950",
+                    "--cuda-device-only", "-S", src, "-o", str(out)],
+                   check=True, capture_output=True, timeout=600)
+    return out.read_text()
+
+
+def _kernels(text, name):
+    """The instruction lines of every kernel whose symbol contains `name` (label to
+    .Lfunc_end), comments and assembler markers dropped."""
+    out = []
+    for m in re.finditer(r"^(_Z\w*" + name + r"\w*):", text, re.M):
+        body = text[m.end():text.index(".Lfunc_end", m.end())]
+        lines = []
+        for l in body.splitlines():
+            l = l.split(";")[0].strip()
+            if l and not l.startswith(".") and not l.endswith(":"):
+                lines.append(l)
+        out.append(lines)
+    assert out, f"no kernel {name}"
+    return out
+
+
+@pytest.fixture(scope="module")
+def epochs_asm(tmp_path_factory):
+    return _asm(os.path.join(ROOT, "ghex_amd", "csrc", "ghx_epochs.hip"),
+                tmp_path_factory.mktemp("asm"))
+
+
+def _releases_are_waited(lines):
+    """Every buffer_wbl2 is system scope and a full `s_waitcnt vmcnt(0)` comes after it before
+    the next store (loads may overlap the write-back; no flag store can overtake it)."""
+    n = 0
+    for i, l in enumerate(lines):
+        if l.startswith("buffer_wbl2"):
+            assert l == "buffer_wbl2 sc0 sc1", l  # system scope
+            j = next(k for k in range(i + 1, len(lines)) if lines[k].startswith("global_store"))
+            assert "s_waitcnt vmcnt(0)" in lines[i + 1:j], lines[i:j + 1]
+            n += 1
+    return n
+
+
+def test_every_release_is_waited_for(epochs_asm):
+    (lines,) = _kernels(epochs_asm, "k_epoch_close")
+    assert _releases_are_waited(lines) >= 1
+    # the open kernel publishes no data (its flags follow reads only): no fences at all
+    (lines,) = _kernels(epochs_asm, "k_epoch_open")
+    assert not [l for l in lines if l.startswith(("buffer_wbl2", "buffer_inv"))]
+
+
+def test_close_kernel_fences_every_xcd(epochs_asm):
+    (lines,) = _kernels(epochs_asm, "k_epoch_close")
+    text = "\n".join(lines)
+    assert "hwreg(HW_REG_XCC_ID" in text
+    # the first memory write of every workgroup ("XCD x written back") comes after the
+    # system-scope release and its wait
+    first_rel = lines.index("buffer_wbl2 sc0 sc1")
+    first_store = next(i for i, l in enumerate(lines) if l.startswith("global_store"))
+    assert first_rel < first_store
+    assert "s_waitcnt vmcnt(0)" in lines[first_rel:first_store]
+    # the system-scope acquire sits behind a full wait, and nothing touches memory after it
+    i = lines.index("buffer_inv sc0 sc1")
+    assert lines[i - 1] == "s_waitcnt vmcnt(0)", lines[i - 3:i + 1]
+    assert not [l for l in lines[i + 1:] if re.match(r"(global|flat|buffer)_", l)]
+    assert lines.count("buffer_inv sc0 sc1") == 1
+
+
+@pytest.mark.parametrize("kernel", ["k_epoch_open", "k_epoch_close"])
+def test_flag_accesses_are_scoped_vector_ops(epochs_asm, kernel):
+    (lines,) = _kernels(epochs_asm, kernel)
+    mem = [l for l in lines if re.match(r"(global|flat|buffer)_(load|store|atomic)", l)]
+    assert not [l for l in mem if l.startswith("flat_")]
+    flags = [l for l in mem if re.match(r"global_(load|store)_dwordx2", l)]
+    assert flags
+    # 8-B flags and words: host-block flags at system scope, device words at agent scope
+    assert all(l.endswith(" sc1") for l in flags), [l for l in flags if not l.endswith(" sc1")]
+    assert any(l.endswith(" sc0 sc1") and "store" in l for l in flags)
+    assert any(l.endswith(" sc0 sc1") and "load" in l for l in flags)
+    # the only other loads: the peer lists from the kernel arguments (read-only)
+    assert all(re.match(r"global_load_ushort", l) for l in mem if l not in flags)
+
+
+@pytest.fixture(scope="module")
+def kernels_asm(tmp_path_factory):
+    return _asm(os.path.join(ROOT, "ghex_amd", "csrc", "ghx_kernels.hip"),
+                tmp_path_factory.mktemp("asmk"))
+
+
+@pytest.mark.parametrize("kernel", ["k_copy", "k_put"])
+def test_peer_writing_kernels_store_through_global_ops(kernels_asm, kernel):
+    bodies = _kernels(kernels_asm, kernel)
+    for lines in bodies:
+        stores = [l for l in lines if re.match(r"(global|flat|buffer)_store", l)]
+        assert stores
+        assert all(l.startswith("global_store") for l in stores), stores[:4]
+        assert not [l for l in stores if " nt" in l], "non-temporal peer stores"

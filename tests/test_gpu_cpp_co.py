@@ -220,7 +220,7 @@ def _shm_name(tag):
 
 @pytest.mark.parametrize("n", [2, 3, 5])
 def test_shm_transport_all_gather_processes_cpu(n):
-    """include/ghex_amd/shm_transport.hpp's setup collective with ranks as PROCESSES (no GPU
+    """tests/cpp/shm_transport.hpp's setup collective with ranks as PROCESSES (no GPU
     calls): 60 all_gather rounds of varying sizes (0..4 KB) with barriers between, every byte of
     every contribution checked on every rank; the segment is unlinked once all have attached."""
     name = _shm_name(f"g{n}")

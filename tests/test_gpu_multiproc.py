@@ -95,3 +95,11 @@ def test_direct_unstructured(world, levels):
     """The direct exchange of an unstructured field (random storage order, halo cells drawn from
     every other rank, levels first): the same plan machinery as the structured one."""
     _run((world, 1, 1), 3000, levels, "udirect")
+
+
+@pytest.mark.parametrize("mode", ["slowdirect", "slowbulk"])
+def test_epoch_failure_reaches_both_sides(mode):
+    """A receiver 5 s late with a 1.5 s epoch timeout: the sender's open wait times out and its
+    wait() raises; the late receiver, whose own waits pass, raises too (the sender marked its
+    done flag FAIL: its writes may have overlapped the receiver's reads) — ADVICE r03."""
+    _run((2, 1, 1), 8, 1, mode)

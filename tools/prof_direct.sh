@@ -5,9 +5,9 @@ O=gpurun_out/prof_direct; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 for r in 0 1; do
   RANK=$r WORLD_SIZE=2 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 timeout -k 10 300 \
-    rocprofv3 --kernel-trace --stats -d $O/r$r -o run -- python3 tests/mp_exchange_worker.py 2 1 1 128 2 40 direct \
+    rocprofv3 --kernel-trace --stats -d $O/r$r -o run --output-format csv -- python3 tests/mp_exchange_worker.py 2 1 1 128 2 40 direct \
     > $O/log$r.txt 2>&1 &
 done
 wait
 tail -2 $O/log0.txt
-find $O -name "*kernel_stats.csv" | head
+python3 tools/parse_prof_direct.py $O > $O/summary.json && head -c 400 $O/summary.json
