@@ -379,6 +379,7 @@ class communication_object
     context* m_ctx;
     options m_opt;
     hipStream_t m_stream = nullptr;
+    bool m_capturing = false;  // the exchange being started is enqueued into a stream capture
     hipEvent_t m_done = nullptr, m_start = nullptr;
     std::vector<hipStream_t> m_lanes;     // pipelined: the peer streams
     std::vector<hipEvent_t> m_lane_done;
@@ -495,6 +496,10 @@ class communication_object
     // attach the plan's epoch flag block (collective over the transport, at plan creation)
     void setup_direct(plan& p)
     {
+        if (m_capturing)
+            throw std::runtime_error("direct exchange: a plan's first exchange sets up IPC handles and flag "
+                                     "blocks collectively and cannot run inside a stream capture; run one "
+                                     "exchange of these fields before capturing");
         auto& t = m_ctx->get_transport();
         const int me = m_ctx->rank(), world = m_ctx->size();
         char hn[256] = {0};
@@ -845,6 +850,8 @@ class communication_object
     {
         if (m_valid) throw std::runtime_error("earlier exchange operation was not finished");
         if (items.empty()) return {};
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        m_capturing = after && hipStreamIsCapturing(after, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
         plan& p = plan_for(items);
         if (after)
         {
