@@ -125,6 +125,8 @@ _SIGS = {
     "ghx_epochs_enqueue": (c_i32, [c_vp, c_i32, c_vp]),
     "ghx_epochs_status": (c_i32, [c_vp, P(c_i32), P(ctypes.c_uint64)]),
     "ghx_epochs_info": (c_i32, [c_vp, P(c_i32), P(c_i32)]),
+    "ghx_epochs_counter": (c_i32, [c_vp, P(c_vp)]),
+    "ghx_exchange_set_parity": (c_i32, [c_vp, c_i32, c_vp, ctypes.c_uint32, P(ctypes.c_int64), c_i32]),
     "ghx_epochs_destroy": (c_i32, [c_vp]),
     "ghx_copier_create": (c_i32, [ctypes.c_uint64, ctypes.c_double, P(c_vp)]),
     "ghx_copier_info": (c_i32, [c_vp, P(c_i32), P(c_i32), P(ctypes.c_float), P(ctypes.c_float),

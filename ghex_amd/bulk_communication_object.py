@@ -112,7 +112,8 @@ def epochs_error(ep, hosts=None, me=None):
         who = f"node-local rank {s}"
         if hosts is not None and me is not None:
             who = f"rank {node_local_group(hosts, me)[0][s]}"
-        return f"{who} failed its own open phase: its writes may have overlapped this rank's reads"
+        return (f"{who} failed an epoch wait: its later writes may have overlapped this rank's "
+                f"reads")
     return f"epoch error code {v}"
 
 
@@ -320,7 +321,7 @@ class BulkCommunicationObject:
 
     def check_epochs(self):
         """Raise if this rank's epochs recorded a failure (a wait timed out: a peer never reached
-        the exchange; or a source failed its own open phase)."""
+        the exchange; or a source failed an epoch wait)."""
         if self._ep is None:
             return
         why = epochs_error(self._ep, self._hosts, self.context.rank())

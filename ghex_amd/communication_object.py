@@ -35,11 +35,15 @@ peer receive buffers (IPC) at the first exchange of a plan and imports the buffe
 receive into; the ONE pack launch then writes each peer message straight into the receiver's
 buffer (lane-linear 16-B stores: dense writes over xGMI between GPUs, where the bulk object's
 field-to-field puts scatter the x-normal faces' 16-B rows), and the receiver unpacks it locally.
-Ordering is the bulk object's stream-ordered device epochs (libghx ghx_epochs_*; the reference's
-access guards, include/ghex/rma/access_guard.hpp:35-140): k_epoch(open) — this rank's receive
-buffers are free (its previous unpack is done) and every target's are — pack — k_epoch(close) —
-this rank's writes are visible and every source's have landed — unpack. No host synchronisation;
-graph-capturable; structured and unstructured fields alike.
+Ordering is stream-ordered device epochs (libghx ghx_epochs_*; the reference's access guards,
+include/ghex/rma/access_guard.hpp:35-140) in ONE launch per exchange: each peer receive buffer
+exists twice and exchange e uses the copy of parity e&1 (chosen on the device from the epoch
+counter, so graph replays alternate), so the copy a source writes at e+1 was last read by this
+rank's unpack of e-1 — done before this rank's close of e, which says so to its sources. Per
+exchange: pack (into copy e&1 of the receivers' buffers) — k_epoch_close1 (this rank's writes
+visible on every XCD, peers signalled, every source's writes and every target's previous unpack
+awaited) — unpack (copy e&1). No host synchronisation; graph-capturable; structured and
+unstructured fields alike.
 """
 from __future__ import annotations
 
@@ -77,6 +81,11 @@ class _ExchangePlan:
                 self.h = None
         except Exception:
             pass
+
+
+def _dbl(size):
+    """Offset of the odd-parity copy of a double-buffered receive buffer (256-B aligned)."""
+    return max(256, (int(size) + 255) // 256 * 256)
 
 
 def route(context, sends, recvs, group=None):
@@ -329,8 +338,14 @@ class CommunicationObject:
                 # self-message: unpack straight from the matching send buffer
                 j = next((i for i, s in enumerate(plan.send)
                           if s["pair"] == x["pair"] and x["rank"] == me and alias), None)
-                recv.append(send[j] if j is not None else
-                            torch.empty(max(1, x["size"]), dtype=torch.uint8, device=device))
+                if j is not None:
+                    recv.append(send[j])
+                elif self.direct and x["rank"] != me:
+                    # direct: a peer's receive buffer exists twice, the copy of each exchange's
+                    # epoch parity (one-launch epochs, _direct_of); the odd copy _dbl bytes on
+                    recv.append(torch.empty(2 * _dbl(x["size"]), dtype=torch.uint8, device=device))
+                else:
+                    recv.append(torch.empty(max(1, x["size"]), dtype=torch.uint8, device=device))
             b = (send, recv)
             self._bufs[key] = b
         return b
@@ -680,7 +695,7 @@ class CommunicationObject:
             h = (ctypes.c_ubyte * 64)()
             off = ctypes.c_uint64()
             _ghx.call("ghx_ipc_export", ctypes.c_void_p(recv[j].data_ptr()), h, ctypes.byref(off))
-            mine.append((x["rank"], x["tag"], x["size"], bytes(h), off.value))
+            mine.append((x["rank"], x["tag"], x["size"], bytes(h), off.value, _dbl(x["size"])))
         allr = self.context.all_gather_object({"host": host, "recv": mine,
                                                "targets": sorted(by_peer)})
         # every rank checks every pair, so all raise together (none is left in a collective)
@@ -695,13 +710,15 @@ class CommunicationObject:
         imports = []
         d = {"sptrs": None, "ep": None, "imports": imports}
         self._direct[id(plan)] = d  # before anything can raise: __del__ closes what was opened
-        for i, (_, tag, size, hb, off) in direct_matches(me, plan.send,
-                                                         {r: a["recv"] for r, a in enumerate(allr)}):
+        send_dbl = [0] * len(plan.send)
+        for i, (_, tag, size, hb, off, dbl) in direct_matches(
+                me, plan.send, {r: a["recv"] for r, a in enumerate(allr)}):
             base, ptr = ctypes.c_void_p(), ctypes.c_void_p()
             _ghx.call("ghx_ipc_import", (ctypes.c_ubyte * 64).from_buffer_copy(hb), off,
                       ctypes.byref(base), ctypes.byref(ptr))
             imports.append(base.value)
             ptrs[i] = ptr.value
+            send_dbl[i] = dbl
         if world > 1:
             # one node-shared flag block per plan and host: the host's lowest rank creates it,
             # the host's other ranks attach (node-local indices); ranks of other hosts take part
@@ -711,18 +728,27 @@ class CommunicationObject:
             srcs = sorted({x["rank"] for x in plan.recv if x["rank"] != me})
             d["ep"] = attach_epochs(self.context, d["hosts"], self.epoch_timeout, srcs,
                                     sorted(by_peer), prefix="dx")
+        if d["ep"] is not None:
+            # one launch of epochs per exchange (ghx_epochs phase 2): the peers' receive buffers
+            # are double-buffered by epoch parity, read on the device from the epoch counter
+            word = ctypes.c_void_p()
+            _ghx.call("ghx_epochs_counter", d["ep"], ctypes.byref(word))
+            recv_dbl = [_dbl(x["size"]) if x["rank"] != me else 0 for x in plan.recv]
+            for direction, add, offs in ((0, 1, send_dbl), (1, 0, recv_dbl)):
+                _ghx.call("ghx_exchange_set_parity", plan.h, direction, word, add,
+                          (ctypes.c_int64 * max(1, len(offs)))(*offs), len(offs))
         d["sptrs"] = _ghx.ptr_array(ptrs)
         return d
 
     def _exchange_direct(self, plan, d, fptrs, nf, rptrs, nr, stream):
         s = stream.cuda_stream
         mixed = self.fuse_self and self.mixed(plan)
-        if d["ep"] is not None:
-            _ghx.call("ghx_epochs_enqueue", d["ep"], 0, s)  # open: buffers free here and there
+        # pack into copy e&1 of the receivers' buffers -> one-launch close (release, signal,
+        # wait, acquire) -> unpack copy e&1 of this rank's
         _ghx.call("ghx_exchange_pack_self" if mixed else "ghx_exchange_pack", plan.h, fptrs, nf,
                   d["sptrs"], len(plan.send), s)
         if d["ep"] is not None:
-            _ghx.call("ghx_epochs_enqueue", d["ep"], 1, s)  # close: every source's writes landed
+            _ghx.call("ghx_epochs_enqueue", d["ep"], 2, s)
         _ghx.call("ghx_exchange_unpack_peers" if mixed else "ghx_exchange_unpack", plan.h, fptrs,
                   nf, rptrs, nr, s)
         import torch
@@ -732,7 +758,7 @@ class CommunicationObject:
 
     def check_epochs(self):
         """Raise if a direct exchange's epochs recorded a failure (a wait timed out: a peer
-        never reached it; or a source failed its own open phase)."""
+        never reached it; or a source failed an epoch wait)."""
         from .bulk_communication_object import epochs_error
         for d in self._direct.values():
             if d["ep"] is None:

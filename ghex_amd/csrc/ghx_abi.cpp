@@ -1206,7 +1206,43 @@ int ghx_exchange_pack_self(const ghx_exchange* ex, void* const* field_ptrs, int3
             if (!send_buffers[i]) throw invalid("null buffer pointer");
             a.buf_ptr[i] = reinterpret_cast<uint64_t>(send_buffers[i]);
         }
+        ex->mixed_parity.apply(a, {}, p.max_buf_slot + 1);
         return launch_self(a, stream, grid_for_tiles(p.n_tiles));
+    });
+}
+
+int ghx_exchange_set_parity(ghx_exchange* ex, int32_t direction, const uint64_t* parity_word,
+                            uint32_t parity_add, const int64_t* offsets, int32_t n_buffers)
+{
+    return guarded([&] {
+        check_ptr(ex, "exchange");
+        if (direction != 0 && direction != 1) throw invalid("direction must be 0 (pack) or 1 (unpack)");
+        const size_t n = direction == 0 ? ex->send.size() : ex->recv.size();
+        parity_cfg cfg;
+        if (parity_word)
+        {
+            if (n_buffers != int32_t(n) || (n && !offsets))
+                throw invalid("one offset per buffer of that direction");
+            cfg.word = parity_word;
+            cfg.add = parity_add & 1u;
+            cfg.offset.assign(offsets, offsets + n);
+            for (int64_t o : cfg.offset)
+                if (o < 0 || o % 256 != 0)
+                    throw invalid("second-copy offsets must be >= 0 and multiples of 256 B");
+        }
+        if (direction == 0)
+        {
+            if (ex->spack) ex->spack->parity = cfg;
+            if (ex->upack) ex->upack->parity = cfg;
+            ex->mixed_parity = cfg;
+        }
+        else
+        {
+            if (ex->sunpack) ex->sunpack->parity = cfg;
+            if (ex->uunpack) ex->uunpack->parity = cfg;
+            if (ex->punpack) ex->punpack->parity = cfg;
+        }
+        return GHX_OK;
     });
 }
 

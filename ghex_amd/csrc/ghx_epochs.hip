@@ -79,10 +79,12 @@ __host__ __device__ inline size_t l_error(int r, int W) { return l_epoch(r, W) +
 __host__ __device__ inline size_t l_open(int r, int t, int W) { return l_epoch(r, W) + 2 + size_t(t); }
 __host__ __device__ inline size_t l_done(int r, int s, int W) { return l_epoch(r, W) + 2 + size_t(W) + size_t(s); }
 inline size_t block_lines(int W) { return 1 + size_t(W) * (2 + 2 * size_t(W)); }
-// device words: line 0 = {epoch in flight, failed epoch}, 1 + x = XCD x written back, go
+// device words: line 0 = {epoch counter, failure mark}, 1 + x = XCD x written back, go, and the
+// one-launch close's arrival count
 constexpr size_t d_rel(int x) { return 1 + size_t(x); }
 constexpr size_t d_go = 1 + kMaxXcc;
-constexpr size_t kDevLines = d_go + 1;
+constexpr size_t d_arrive = d_go + 1;
+constexpr size_t kDevLines = d_arrive + 1;
 
 __device__ __forceinline__ uint64_t* at(uint64_t* f, size_t line) { return f + line * 8; }
 
@@ -219,13 +221,78 @@ __global__ __launch_bounds__(64) void k_epoch_close(epoch_args a)
     }
     else if (a.n_src > 0)
     {
-        if (!wave_wait_dev(lane == 0 ? at(dv, d_go) : nullptr, e, a.timeout_ticks) && lane == 0)
+        // the leader sets go within its own bounded waits (2 x timeout at most): a follower
+        // that outlasts 3 x timeout means the leader never ran
+        if (!wave_wait_dev(lane == 0 ? at(dv, d_go) : nullptr, e, 3 * a.timeout_ticks) && lane == 0)
             sys_store(at(f, l_error(R, W)), kErrFence);
     }
     // what the sources wrote is read by the kernels after this one: no stale line in this XCD's
     // L2 (nor this CU's L1; the next launch invalidates the other CUs' L1s). A rank without
     // sources reads nothing new and skips it.
     if (a.n_src > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+}
+// One-launch close (phase 2) for exchanges whose receive memory is double-buffered by epoch
+// parity (the direct exchange: ghx_exchange_set_parity). Epoch e = counter + 1; the data launch
+// before it wrote copy e&1 of each target's buffers, the unpack after it reads copy e&1 of this
+// rank's. No open phase: the copy a source writes at e+1 was last read by this rank's unpack of
+// e-1, which ran before this close (stream order), so this close tells its sources so
+// (open[s][R] = e) together with done[t][R] = e, and waits for both from its peers:
+//   every workgroup: system-scope release (if it has targets) -> "XCD x written back"; arrive;
+//   leader: every XCD written back and every workgroup arrived (all have read the counter);
+//     done[t][R] = e (FAIL after an earlier failure of R) and open[s][R] = e; wait until
+//     done[R][s] >= e (the sources' writes of e are in copy e&1) and open[R][t] >= e (the
+//     targets are done reading the copy R writes at e+1); counter = e; go;
+//   every workgroup after go: system-scope acquire.
+__global__ __launch_bounds__(64) void k_epoch_close1(epoch_args a)
+{
+    const int lane = int(threadIdx.x);
+    const int R = a.rank, W = a.world;
+    uint64_t* f = a.flags;
+    uint64_t* dv = a.dev;
+    if (a.n_tgt > 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    const uint64_t e = dev_load(at(dv, 0)) + 1;
+    const bool failed_before = dev_load(at(dv, 0) + 1) != 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+    {
+        if (a.n_tgt > 0) dev_store(at(dv, d_rel(int(xcc_id()))), e);
+        __hip_atomic_fetch_add(at(dv, d_arrive), uint64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (blockIdx.x == 0)
+    {
+        uint64_t err = 0, seen = 0;
+        if (a.n_tgt > 0 &&
+            !wave_wait_dev(lane < a.n_xcc ? at(dv, d_rel(lane)) : nullptr, e, a.timeout_ticks))
+            err = kErrFence;
+        if (!err && !wave_wait_dev(lane == 0 ? at(dv, d_arrive) : nullptr, e * gridDim.x, a.timeout_ticks))
+            err = kErrFence;
+        if (err && lane == 0) sys_store(at(f, l_error(R, W)), err);
+        const uint64_t mark = (failed_before || err) ? kFail : 0;
+        if (lane < a.n_tgt) sys_store(at(f, l_done(a.tgt[lane], R, W)), e | mark);
+        if (lane < a.n_src) sys_store(at(f, l_open(a.src[lane], R, W)), e);
+        if (!err)
+        {
+            // lanes [0, n_src): the sources' done flags; [n_src, n_src + n_tgt): the targets'
+            const int ns = a.n_src, nt = a.n_tgt;
+            uint64_t* flag = lane < ns ? at(f, l_done(R, a.src[lane], W))
+                             : lane < ns + nt ? at(f, l_open(R, a.tgt[lane - ns], W)) : nullptr;
+            err = wave_wait(at(f, l_error(R, W)), flag, e, a.timeout_ticks, kErrClose, &seen);
+            const bool bad = !err && lane < ns && (seen & kFail);
+            const uint64_t m = __ballot(bad);
+            if (m && lane == int(__builtin_ctzll(m)))
+                sys_store(at(f, l_error(R, W)), kErrPeer | (uint64_t(a.src[lane]) << 8));
+        }
+        if (lane == 0)
+        {
+            if (err) dev_store(at(dv, 0) + 1, 1);  // later done flags carry FAIL
+            dev_store(at(dv, 0), e);
+            dev_store(at(dv, d_go), e);
+            sys_store(at(f, l_epoch(R, W)), e);  // the host's view (ghx_epochs_status)
+        }
+    }
+    else if (!wave_wait_dev(lane == 0 ? at(dv, d_go) : nullptr, e, 4 * a.timeout_ticks) && lane == 0)
+        sys_store(at(f, l_error(R, W)), kErrFence);  // the leader never ran (its waits are bounded)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
 }
 }  // namespace
 }  // namespace ghx
@@ -240,6 +307,7 @@ struct ghx_epochs
     bool registered = false;
     uint64_t* dev = nullptr;
     int fence_groups = 0;
+    int mode = -1;  // 0: open + close (phases 0, 1); 1: one-launch close (phase 2)
     epoch_args args{};
     ~ghx_epochs()
     {
@@ -366,18 +434,28 @@ int ghx_epochs_peers(ghx_epochs* ep, const int32_t* sources, int32_t n_sources,
     });
 }
 
-// phase 0: open (before this rank's data launch), 1: close (after it). Two launches per exchange.
-int ghx_epochs_enqueue(const ghx_epochs* ep, int32_t phase, ghx_stream stream)
+// phase 0: open (before this rank's data launch), 1: close (after it) — two launches per
+// exchange; phase 2: the one-launch close of double-buffered exchanges (after the data launch,
+// before the unpack). An object uses phases 0/1 or phase 2, never both.
+int ghx_epochs_enqueue(ghx_epochs* ep, int32_t phase, ghx_stream stream)
 {
     return guarded([&] {
         if (!ep) throw invalid("null epochs");
-        if (phase != 0 && phase != 1) throw invalid("phase must be 0 (open) or 1 (close)");
+        if (phase < 0 || phase > 2) throw invalid("phase must be 0 (open), 1 (close) or 2 (one-launch close)");
+        const int mode = phase == 2 ? 1 : 0;
+        if (ep->mode >= 0 && ep->mode != mode)
+            throw invalid("an epochs object runs either open/close (phases 0, 1) or the one-launch close (2)");
+        if (phase == 2 && ep->args.n_src + ep->args.n_tgt > kMaxPeers)
+            throw invalid("the one-launch close waits on at most 63 sources + targets");
+        ep->mode = mode;
         const auto s = static_cast<hipStream_t>(stream);
         if (phase == 1 && ep->args.n_src == 0 && ep->args.n_tgt == 0) return GHX_OK;  // no peers
         if (phase == 0)
             hipLaunchKernelGGL(k_epoch_open, dim3(1), dim3(64), 0, s, ep->args);
-        else
+        else if (phase == 1)
             hipLaunchKernelGGL(k_epoch_close, dim3(ep->fence_groups), dim3(64), 0, s, ep->args);
+        else
+            hipLaunchKernelGGL(k_epoch_close1, dim3(ep->fence_groups), dim3(64), 0, s, ep->args);
         if (hipGetLastError() != hipSuccess) throw hip_error("k_epoch launch");
         return GHX_OK;
     });
@@ -385,7 +463,7 @@ int ghx_epochs_enqueue(const ghx_epochs* ep, int32_t phase, ghx_stream stream)
 
 // *error: 0, 1 / 2 when a wait of the open / close phase timed out (a peer never reached the
 // exchange), 3 when the close kernel's workgroups did not reach every XCD in time, 4 | s << 8
-// when source s (node-local index) failed its own open phase; *epoch: this rank's exchange
+// when source s (node-local index) failed an epoch wait; *epoch: this rank's exchange
 // counter. Host reads of the coherent flag block.
 int ghx_epochs_status(const ghx_epochs* ep, int32_t* error, uint64_t* epoch)
 {
@@ -405,6 +483,18 @@ int ghx_epochs_info(const ghx_epochs* ep, int32_t* n_xcc, int32_t* fence_groups)
         if (!ep) throw invalid("null epochs");
         if (n_xcc) *n_xcc = ep->args.n_xcc;
         if (fence_groups) *fence_groups = ep->fence_groups;
+        return GHX_OK;
+    });
+}
+
+// The device word holding this rank's epoch counter: the parity word of double-buffered
+// launches (ghx_exchange_set_parity): a pack before the phase-2 close of epoch e reads e - 1
+// (parity_add 1), an unpack after it reads e (parity_add 0).
+int ghx_epochs_counter(const ghx_epochs* ep, const uint64_t** word)
+{
+    return guarded([&] {
+        if (!ep || !word) throw invalid("null argument");
+        *word = ep->dev;
         return GHX_OK;
     });
 }

@@ -31,6 +31,7 @@ struct exchange_plan
     int mixed_max_field_slot = -1;  // the highest field slot mixed_comp's segments name
     std::unique_ptr<splan> punpack;
     bool mixed = false;
+    parity_cfg mixed_parity;  // the mixed pack launch's double-buffered send buffers (direct)
     int32_t n_items = 0;
     mutable int self_ok = -1;  // lazily checked: may pack and unpack be fused (all self)?
 

@@ -133,15 +133,42 @@ struct alignas(16) seg_u
 };
 static_assert(sizeof(seg_u) == 96, "seg_u layout");
 
-// Kernel arguments (passed by value: <= 1.1 KB of kernarg).
+// Kernel arguments (passed by value: <= 1.7 KB of kernarg).
 struct kargs
 {
     const void* segs;
     const void* segs2;         // fused self exchange: the unpack segments (1:1 with segs)
     const uint32_t* tile_seg;  // per tile: {segment index, tile index within the segment}
     uint32_t n_tiles;
+    uint32_t parity_add;       // double-buffered launches: parity = (*parity_word + add) & 1
+    const uint64_t* parity_word;  // null: single-buffered (the kernels' plain variants)
     uint64_t field_ptr[GHX_MAX_SLOTS];
     uint64_t buf_ptr[GHX_MAX_SLOTS];
+    int64_t dbl_off[GHX_MAX_SLOTS];  // per buffer slot: byte offset of its odd-parity copy (0: none)
+};
+
+// Double-buffered buffers (the direct exchange's one-launch epochs, ghx_epochs.hip): a buffer
+// exists twice, its odd-parity copy `offset` bytes after the even one, and a launch uses the copy
+// of the exchange's parity, read on the device from the epoch counter (so that a captured graph
+// alternates on replay). Per caller buffer index: the offset (0 = one copy only).
+struct parity_cfg
+{
+    const uint64_t* word = nullptr;
+    uint32_t add = 0;
+    std::vector<int64_t> offset;
+    // fill a launch's parity fields; map: local slot -> caller buffer index (empty: identity)
+    void apply(kargs& a, const std::vector<int32_t>& map, int n_identity) const
+    {
+        if (!word) return;
+        a.parity_word = word;
+        a.parity_add = add;
+        const int n = map.empty() ? n_identity : int(map.size());
+        for (int i = 0; i < n; ++i)
+        {
+            const size_t c = size_t(map.empty() ? i : map[size_t(i)]);
+            a.dbl_off[i] = c < offset.size() ? offset[c] : 0;
+        }
+    }
 };
 
 // thread-local last error

@@ -430,10 +430,21 @@ __device__ __forceinline__ void copy_any(const Seg& s, char* field, char* buf, u
 // RUNS (unstructured only): every segment of the plan takes the run path (copy_runs); the host
 // (uplan::execute) launches this variant only when runs_ok holds for all of them, so the
 // general path's registers do not weigh on it and vice versa.
-template<bool PACK, typename Seg, bool RUNS = false>
+// DBL (double-buffered buffers, the direct exchange's one-launch epochs): the launch uses, for
+// every buffer slot with a second copy, the copy of this exchange's parity, read once per
+// workgroup from the epoch counter in device memory (a captured graph alternates on replay).
+__device__ __forceinline__ bool odd_parity(const kargs& a)
+{
+    return ((__hip_atomic_load(a.parity_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+             a.parity_add) & 1) != 0;
+}
+
+template<bool PACK, typename Seg, bool RUNS = false, bool DBL = false>
 __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
 {
     const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
+    bool odd = false;
+    if constexpr (DBL) odd = odd_parity(a);
     for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
     {
         const uint32_t si = a.tile_seg[2 * t];
@@ -443,6 +454,8 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         const uint32_t end = min(start + s.tile_bytes, s.bytes);
         char* field = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
         char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
+        if constexpr (DBL)
+            if (odd) buf += a.dbl_off[s.buf_slot];
         if constexpr (RUNS)
         {
             if (s.row_bytes == 8) copy_runs<PACK, 8>(s, field, buf, start, end);
@@ -508,10 +521,13 @@ __device__ __forceinline__ void self_forward(const seg_s& s, const seg_s& q,
 // it writes the halo from the registers it stored the buffer from (self_forward), no barrier.
 // Otherwise the workgroup packs its tile (field interior -> buffer), passes a workgroup barrier
 // (its own stores are visible to its own waves), then unpacks the same bytes (buffer -> halo).
+template<bool DBL = false>
 __global__ __launch_bounds__(kBlock) void k_self(kargs a)
 {
     const seg_s* __restrict__ ps = static_cast<const seg_s*>(a.segs);
     const seg_s* __restrict__ us = static_cast<const seg_s*>(a.segs2);
+    bool odd = false;
+    if constexpr (DBL) odd = odd_parity(a);
     for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
     {
         const uint32_t si = a.tile_seg[2 * t];
@@ -523,6 +539,8 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
         char* field_p = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
         char* field_u = reinterpret_cast<char*>(a.field_ptr[q.field_slot]);
         char* buf = reinterpret_cast<char*>(a.buf_ptr[s.buf_slot]) + s.buf_off;
+        if constexpr (DBL)
+            if (odd) buf += a.dbl_off[s.buf_slot];
         int wp = min(int(s.wlog2), ptr_wlog2(reinterpret_cast<uint64_t>(field_p)));
         wp = min(wp, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
         int wu = min(int(q.wlog2), ptr_wlog2(reinterpret_cast<uint64_t>(field_u)));
@@ -678,7 +696,12 @@ int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (direction == 0) launch((k_copy<true, seg_s>), grid, s, a);
+    if (a.parity_word)
+    {
+        if (direction == 0) launch((k_copy<true, seg_s, false, true>), grid, s, a);
+        else launch((k_copy<false, seg_s, false, true>), grid, s, a);
+    }
+    else if (direction == 0) launch((k_copy<true, seg_s>), grid, s, a);
     else launch((k_copy<false, seg_s>), grid, s, a);
     return launched("structured");
 }
@@ -686,7 +709,8 @@ int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid
 int launch_self(const kargs& a, void* stream, uint32_t grid)
 {
     if (a.n_tiles == 0) return GHX_OK;
-    launch(k_self, grid, static_cast<hipStream_t>(stream), a);
+    if (a.parity_word) launch(k_self<true>, grid, static_cast<hipStream_t>(stream), a);
+    else launch(k_self<false>, grid, static_cast<hipStream_t>(stream), a);
     return launched("self-exchange");
 }
 
@@ -701,7 +725,14 @@ int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t gr
 {
     if (a.n_tiles == 0) return GHX_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (runs && direction == 0) launch((k_copy<true, seg_u, true>), grid, s, a);
+    if (a.parity_word)
+    {
+        if (runs && direction == 0) launch((k_copy<true, seg_u, true, true>), grid, s, a);
+        else if (runs) launch((k_copy<false, seg_u, true, true>), grid, s, a);
+        else if (direction == 0) launch((k_copy<true, seg_u, false, true>), grid, s, a);
+        else launch((k_copy<false, seg_u, false, true>), grid, s, a);
+    }
+    else if (runs && direction == 0) launch((k_copy<true, seg_u, true>), grid, s, a);
     else if (runs) launch((k_copy<false, seg_u, true>), grid, s, a);
     else if (direction == 0) launch((k_copy<true, seg_u>), grid, s, a);
     else launch((k_copy<false, seg_u>), grid, s, a);

@@ -485,6 +485,7 @@ int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
         a.n_tiles = nt;
         fill_slots(a.field_ptr, fptr, fm, max_field_slot + 1, "field");
         fill_slots(a.buf_ptr, bptr, bm, max_buf_slot + 1, "buffer");
+        parity.apply(a, bm, max_buf_slot + 1);
         return launch_structured(a, direction, stream, grid_for_tiles(nt));
     };
     int rc = run(dev, n_tiles, fmap, bmap);
@@ -715,12 +716,14 @@ int uplan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
         a.n_tiles = nt;
         fill_slots(a.field_ptr, fptr, fm, max_field_slot + 1, "field");
         fill_slots(a.buf_ptr, bptr, bm, max_buf_slot + 1, "buffer");
+        parity.apply(a, bm, max_buf_slot + 1);
         // the run-path kernel when every segment qualifies with these pointers: flagged by the
-        // planner, whole 16-B chunks per tile, 16-B aligned buffer ranges, field base aligned to L
+        // planner, whole 16-B chunks per tile, 16-B aligned buffer ranges (both copies of a
+        // double-buffered one), field base aligned to L
         bool runs = !hs.empty();
         for (const seg_u& s : hs)
             runs = runs && s.runs && s.tile_bytes % 16 == 0 &&
-                   (a.buf_ptr[s.buf_slot] + s.buf_off) % 16 == 0 &&
+                   (a.buf_ptr[s.buf_slot] + s.buf_off) % 16 == 0 && a.dbl_off[s.buf_slot] % 16 == 0 &&
                    a.field_ptr[s.field_slot] % s.row_bytes == 0;
         return launch_unstructured(a, direction, stream, grid_for_tiles(nt), runs);
     };

@@ -65,6 +65,7 @@ struct splan
     device_tables dev;
     std::vector<int32_t> fmap, bmap;             // the first group's slot maps (empty: identity)
     std::vector<std::unique_ptr<slot_group<seg_s>>> more;  // further launch groups
+    parity_cfg parity;                           // double-buffered buffers (direct exchange)
     bool grouped() const { return !fmap.empty() || !bmap.empty() || !more.empty(); }
     uint32_t total_tiles() const;
     splan(const ghx_pack_entry* entries, int n_entries, int direction);
@@ -84,6 +85,7 @@ struct uplan
     std::vector<seg_u> host_segs;  // for the launch-time choice of the run-path kernel
     std::vector<int32_t> fmap, bmap;
     std::vector<std::unique_ptr<slot_group<seg_u>>> more;
+    parity_cfg parity;
     bool grouped() const { return !fmap.empty() || !bmap.empty() || !more.empty(); }
     uint32_t total_tiles() const;
     uplan(const ghx_upack_entry* entries, int n_entries, int direction);

@@ -60,7 +60,7 @@ inline std::string epochs_error_text(std::int32_t err)
     }
     if ((err & 0xff) == 4)
         return "node-local rank " + std::to_string(err >> 8) +
-               " failed its own open phase: its writes may have overlapped this rank's reads";
+               " failed an epoch wait: its later writes may have overlapped this rank's reads";
     return "epoch error code " + std::to_string(err);
 }
 
@@ -334,7 +334,8 @@ struct communication_options
     int max_streams = 4;
     // direct (one process per rank, node-local peers, device buffers): the pack launch writes
     // each peer message straight into the receiver's buffer (IPC mapping; xGMI between GPUs),
-    // device epochs (ghx_epochs_*) order it, the receiver unpacks locally — no transport step.
+    // device epochs (ghx_epochs_*: one close launch per exchange, the receive buffers double-
+    // buffered by epoch parity) order it, the receiver unpacks locally — no transport step.
     // Setup at a plan's first exchange: receive buffers exported and imported over the
     // transport's all_gather (collective). The Python CommunicationObject(direct=True).
     bool direct = false;
@@ -523,12 +524,13 @@ class communication_object
             detail::put(mine, b.size);
             mine.insert(mine.end(), reinterpret_cast<char*>(h), reinterpret_cast<char*>(h) + 64);
             detail::put(mine, off);
+            detail::put(mine, dbl_of(b.size));  // the odd-parity copy's offset
         }
         const auto all = t.all_gather(mine);
         struct entry
         {
             std::int32_t src, tag;
-            std::uint64_t size, off;
+            std::uint64_t size, off, dbl;
             unsigned char h[64];
         };
         std::vector<std::string> hosts(static_cast<std::size_t>(world));
@@ -554,6 +556,7 @@ class communication_object
                 std::memcpy(e.h, in.data() + pos, 64);
                 pos += 64;
                 e.off = detail::get<std::uint64_t>(in, pos);
+                e.dbl = detail::get<std::uint64_t>(in, pos);
                 recv_of[std::size_t(r)].push_back(e);
             }
         }
@@ -566,6 +569,7 @@ class communication_object
                                              " (host " + hosts[std::size_t(e.src)] + ") sends to rank " +
                                              std::to_string(r) + " (host " + hosts[std::size_t(r)] + ")");
         p.dsptr = p.sptr;
+        std::vector<std::int64_t> send_dbl(p.send.size(), 0);
         std::map<int, std::vector<std::size_t>> by_peer;
         for (std::size_t i = 0; i < p.send.size(); ++i)
             if (p.send[i].rank != me) by_peer[p.send[i].rank].push_back(i);
@@ -596,6 +600,7 @@ class communication_object
                 check_ghx(ghx_ipc_import(e.h, e.off, &base, &ptr), "ghx_ipc_import");
                 p.imports.push_back(base);
                 p.dsptr[idx[k]] = ptr;
+                send_dbl[idx[k]] = std::int64_t(e.dbl);
             }
         }
         if (world > 1)
@@ -635,11 +640,26 @@ class communication_object
             std::sort(srcs.begin(), srcs.end());
             std::sort(tgts.begin(), tgts.end());
             if (p.ep)
+            {
                 check_ghx(ghx_epochs_peers(p.ep, srcs.data(), std::int32_t(srcs.size()), tgts.data(),
                                            std::int32_t(tgts.size())),
                           "ghx_epochs_peers");
+                // one epoch launch per exchange: the peers' receive buffers are double-buffered
+                // by epoch parity, chosen on the device from the epoch counter
+                const std::uint64_t* word = nullptr;
+                check_ghx(ghx_epochs_counter(p.ep, &word), "ghx_epochs_counter");
+                std::vector<std::int64_t> recv_dbl;
+                for (auto& b : p.recv) recv_dbl.push_back(b.rank != me ? std::int64_t(dbl_of(b.size)) : 0);
+                check_ghx(ghx_exchange_set_parity(p.ex, 0, word, 1, send_dbl.data(), std::int32_t(send_dbl.size())),
+                          "ghx_exchange_set_parity");
+                check_ghx(ghx_exchange_set_parity(p.ex, 1, word, 0, recv_dbl.data(), std::int32_t(recv_dbl.size())),
+                          "ghx_exchange_set_parity");
+            }
         }
     }
+
+    // the odd-parity copy of a double-buffered (direct) receive buffer starts this far in
+    static std::uint64_t dbl_of(std::uint64_t size) { return std::max<std::uint64_t>(256, (size + 255) / 256 * 256); }
 
     // tag offsets per distinct pattern container in argument order (:540-549) are assigned in
     // start(); here only the per-field description
@@ -759,7 +779,9 @@ class communication_object
                         b.owned = false;
                     }
             }
-            if (!b.data) check_hip(hipMalloc(&b.data, std::max<std::uint64_t>(1, b.size)), "hipMalloc(recv buffer)");
+            // direct: a peer's receive buffer exists twice (one-launch epochs, setup_direct)
+            const std::uint64_t bytes = m_opt.direct && b.rank != me ? 2 * dbl_of(b.size) : std::max<std::uint64_t>(1, b.size);
+            if (!b.data) check_hip(hipMalloc(&b.data, bytes), "hipMalloc(recv buffer)");
         }
         bool all_self = !m_opt.self_through_transport;
         for (auto* v : {&p->send, &p->recv})
@@ -866,15 +888,14 @@ class communication_object
             check_ghx(ghx_exchange_self(p.ex, fptrs.data(), nf, p.sptr.data(), ns, m_stream), "ghx_exchange_self");
         else if (m_opt.direct)
         {
-            // open (buffers free here and at every receiver) -> pack into the receivers'
-            // buffers -> close (every sender's pack landed) -> local unpack
-            if (p.ep) check_ghx(ghx_epochs_enqueue(p.ep, 0, m_stream), "ghx_epochs_enqueue(open)");
+            // pack into copy e&1 of the receivers' buffers -> one-launch close (every sender's
+            // pack landed, every receiver done with the copy of e+1) -> unpack copy e&1
             if (p.mixed)
                 check_ghx(ghx_exchange_pack_self(p.ex, fptrs.data(), nf, p.dsptr.data(), ns, m_stream),
                           "ghx_exchange_pack_self");
             else
                 check_ghx(ghx_exchange_pack(p.ex, fptrs.data(), nf, p.dsptr.data(), ns, m_stream), "ghx_exchange_pack");
-            if (p.ep) check_ghx(ghx_epochs_enqueue(p.ep, 1, m_stream), "ghx_epochs_enqueue(close)");
+            if (p.ep) check_ghx(ghx_epochs_enqueue(p.ep, 2, m_stream), "ghx_epochs_enqueue(close)");
             if (p.mixed)
                 check_ghx(ghx_exchange_unpack_peers(p.ex, fptrs.data(), nf, p.rptr.data(), nr, m_stream),
                           "ghx_exchange_unpack_peers");

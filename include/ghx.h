@@ -397,6 +397,16 @@ int ghx_exchange_pack_self(const ghx_exchange* ex, void* const* field_ptrs, int3
 int ghx_exchange_unpack_peers(const ghx_exchange* ex, void* const* field_ptrs, int32_t n_fields,
                               void* const* recv_buffers, int32_t n_recv, ghx_stream stream);
 
+/* Double-buffered buffers (the direct exchange's one-launch epochs, ghx_epochs_enqueue phase 2):
+ * every later pack (direction 0: ghx_exchange_pack, _pack_self) or unpack (1: ghx_exchange_unpack,
+ * _unpack_peers) launch of `ex` uses, for buffer i with offsets[i] != 0, the copy at
+ * buffer_ptr + offsets[i] when (*parity_word + parity_add) is odd, read on the device at launch
+ * (a captured graph alternates on replay). offsets: one per buffer of that direction, multiples
+ * of 256 B (0 = one copy). parity_word = NULL restores single buffers. The reference has no
+ * equivalent (its RMA path puts field to field, include/ghex/structured/rma_put.hpp:204-245). */
+int ghx_exchange_set_parity(ghx_exchange* ex, int32_t direction, const uint64_t* parity_word,
+                            uint32_t parity_add, const int64_t* offsets, int32_t n_buffers);
+
 /* ------------------------------------------------------------------------------------------
  * Zero-copy put between node-local GPUs. Replaces the reference's RMA path:
  * bulk_communication_object (include/ghex/bulk_communication_object.hpp:206-704), the
@@ -445,7 +455,7 @@ int ghx_put_destroy(ghx_put* put);
  * No host synchronisation, no barrier; the epoch counter lives in memory, so the sequence can
  * be captured into a graph. Waits are bounded: ghx_epochs_status reports 0, 1 / 2 (a wait of
  * the open / close phase timed out), 3 (the close kernel did not reach every XCD in time) or
- * 4 | s << 8 (source s failed its own open phase: its writes may have overlapped this rank's
+ * 4 | s << 8 (source s failed an epoch wait: its later writes may have overlapped this rank's
  * reads). After a nonzero status the object is broken (every later wait returns at once). */
 typedef struct ghx_epochs ghx_epochs;
 int ghx_epochs_create(const char* name, int32_t create, int32_t world, int32_t rank,
@@ -453,9 +463,15 @@ int ghx_epochs_create(const char* name, int32_t create, int32_t world, int32_t r
 int ghx_epochs_unlink(const char* name);
 int ghx_epochs_peers(ghx_epochs* ep, const int32_t* sources, int32_t n_sources,
                      const int32_t* targets, int32_t n_targets);
-int ghx_epochs_enqueue(const ghx_epochs* ep, int32_t phase, ghx_stream stream);
+int ghx_epochs_enqueue(ghx_epochs* ep, int32_t phase, ghx_stream stream);
 int ghx_epochs_status(const ghx_epochs* ep, int32_t* error, uint64_t* epoch);
 int ghx_epochs_info(const ghx_epochs* ep, int32_t* n_xcc, int32_t* fence_groups);
+/* Phase 2 (one launch per exchange) is for receive memory double-buffered by epoch parity
+ * (ghx_exchange_set_parity with the word ghx_epochs_counter returns): data launch (copy e&1 of
+ * the targets') -> ghx_epochs_enqueue(ep, 2, stream) -> unpack (copy e&1 of this rank's). The
+ * close tells the sources that this rank's previous unpack is done, which is what the open
+ * phase is for otherwise. An object runs phases 0/1 or phase 2, not both. */
+int ghx_epochs_counter(const ghx_epochs* ep, const uint64_t** word);
 int ghx_epochs_destroy(ghx_epochs* ep);
 
 /* ------------------------------------------------------------------------------------------

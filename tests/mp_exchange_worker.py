@@ -191,9 +191,14 @@ def main():
 def slow_peer(mode, rank, world, N, Hw, parts):
     """Modes slowdirect / slowbulk (an epoch failure must reach both sides): after
     one good exchange, rank 1 arrives 5 s late at the second one while the epoch timeout is
-    1.5 s. Rank 0's open wait times out — its data launch still writes into rank 1's memory —
-    so rank 0 must raise the open-phase timeout and rank 1, whose own waits pass, must raise that
-    rank 0 failed its open phase (the FAIL mark on rank 0's done flag). Exit 0 when both do."""
+    1.5 s.
+    slowbulk (open + close): rank 0's open wait times out — its puts still write into rank 1's
+      halos — so rank 0 raises the open-phase timeout and rank 1, whose own waits pass, raises
+      that rank 0 failed (the FAIL mark on rank 0's done flag).
+    slowdirect (one-launch close, double-buffered receive buffers): rank 0's close times out;
+      its pack wrote the copy rank 1 was not reading, so rank 1's second exchange is valid and
+      raises nothing; at the third exchange rank 0's done flag carries FAIL and rank 1 raises.
+    Exit 0 when every rank raised (or not) as expected."""
     import time
 
     import torch
@@ -222,13 +227,26 @@ def slow_peer(mode, rank, world, N, Hw, parts):
     dist.barrier()
     if rank == 1:
         time.sleep(5.0)
-    err = ""
-    try:
-        ex().wait()
-    except RuntimeError as e:
-        err = str(e)
-    want = "open phase timed out" if rank == 0 else "failed its own open phase"
-    ok = want in err
+    def attempt():
+        try:
+            ex().wait()
+            return ""
+        except RuntimeError as e:
+            return str(e)
+    err = attempt()
+    if mode == "slowbulk":
+        want = "open phase timed out" if rank == 0 else "failed an epoch wait"
+        ok = want in err
+    else:
+        ok = ("close phase timed out" in err) if rank == 0 else err == ""
+        if rank == 1 and ok:  # the late rank's halos are all valid
+            exp = H.expected_linear_halo(a, dom, N, Hw, gl)
+            ok = bool((base.cpu().numpy() == exp).all())
+        torch.cuda.synchronize()
+        dist.barrier()
+        err3 = attempt()
+        ok = ok and ("failed an epoch wait" in err3 if rank == 1 else err3 != "")
+        err = err + " | third: " + err3
     print(f"{mode} rank {rank}: {'ok' if ok else 'WRONG'}: {err or 'no error raised'}", flush=True)
     t = torch.tensor([0 if ok else 1])
     dist.all_reduce(t)

@@ -70,7 +70,7 @@ def test_epoch_error_codes_decode():
     hosts = ["a", "b", "a", "a"]
     try:
         for code, text in ((0, None), (1, "open phase timed out"), (2, "close phase timed out"),
-                           (3, "every XCD"), (4 | (1 << 8), "rank 2 failed its own open")):
+                           (3, "every XCD"), (4 | (1 << 8), "rank 2 failed an epoch wait")):
             _ghx.call = fake(code)
             got = B.epochs_error(ctypes.c_void_p(1), hosts, 0)
             assert (got is None) if text is None else (text in got), (code, got)

@@ -57,6 +57,11 @@ def epochs_asm(tmp_path_factory):
                 tmp_path_factory.mktemp("asm"))
 
 
+def _full_wait(line):
+    """An s_waitcnt that waits for every outstanding vector-memory operation."""
+    return re.match(r"s_waitcnt\b.*\bvmcnt\(0\)", line) is not None
+
+
 def _releases_are_waited(lines):
     """Every buffer_wbl2 is system scope and a full `s_waitcnt vmcnt(0)` comes after it before
     the next store (loads may overlap the write-back; no flag store can overtake it)."""
@@ -65,21 +70,23 @@ def _releases_are_waited(lines):
         if l.startswith("buffer_wbl2"):
             assert l == "buffer_wbl2 sc0 sc1", l  # system scope
             j = next(k for k in range(i + 1, len(lines)) if lines[k].startswith("global_store"))
-            assert "s_waitcnt vmcnt(0)" in lines[i + 1:j], lines[i:j + 1]
+            assert any(_full_wait(l) for l in lines[i + 1:j]), lines[i:j + 1]
             n += 1
     return n
 
 
-def test_every_release_is_waited_for(epochs_asm):
-    (lines,) = _kernels(epochs_asm, "k_epoch_close")
+@pytest.mark.parametrize("close", ["k_epoch_closeE", "k_epoch_close1"])
+def test_every_release_is_waited_for(epochs_asm, close):
+    (lines,) = _kernels(epochs_asm, close)
     assert _releases_are_waited(lines) >= 1
     # the open kernel publishes no data (its flags follow reads only): no fences at all
     (lines,) = _kernels(epochs_asm, "k_epoch_open")
     assert not [l for l in lines if l.startswith(("buffer_wbl2", "buffer_inv"))]
 
 
-def test_close_kernel_fences_every_xcd(epochs_asm):
-    (lines,) = _kernels(epochs_asm, "k_epoch_close")
+@pytest.mark.parametrize("close", ["k_epoch_closeE", "k_epoch_close1"])
+def test_close_kernel_fences_every_xcd(epochs_asm, close):
+    (lines,) = _kernels(epochs_asm, close)
     text = "\n".join(lines)
     assert "hwreg(HW_REG_XCC_ID" in text
     # the first memory write of every workgroup ("XCD x written back") comes after the
@@ -87,19 +94,30 @@ def test_close_kernel_fences_every_xcd(epochs_asm):
     first_rel = lines.index("buffer_wbl2 sc0 sc1")
     first_store = next(i for i, l in enumerate(lines) if l.startswith("global_store"))
     assert first_rel < first_store
-    assert "s_waitcnt vmcnt(0)" in lines[first_rel:first_store]
-    # the system-scope acquire sits behind a full wait, and nothing touches memory after it
-    i = lines.index("buffer_inv sc0 sc1")
-    assert lines[i - 1] == "s_waitcnt vmcnt(0)", lines[i - 3:i + 1]
-    assert not [l for l in lines[i + 1:] if re.match(r"(global|flat|buffer)_", l)]
-    assert lines.count("buffer_inv sc0 sc1") == 1
+    assert any(_full_wait(l) for l in lines[first_rel:first_store])
+    # every system-scope acquire sits behind a full wait and ends its path (the next
+    # instruction is s_endpgm: nothing touches memory after it); the one-launch close ends every
+    # path with it, the two-launch close those of ranks with sources
+    invs = [i for i, l in enumerate(lines) if l.startswith("buffer_inv")]
+    assert invs
+    for i in invs:
+        assert lines[i] == "buffer_inv sc0 sc1" and _full_wait(lines[i - 1]), lines[i - 3:i + 1]
+        assert lines[i + 1] == "s_endpgm", lines[i:i + 3]
+    if close == "k_epoch_close1":
+        ends = [i for i, l in enumerate(lines) if l == "s_endpgm"]
+        assert all(lines[i - 1] == "buffer_inv sc0 sc1" for i in ends)
 
 
-@pytest.mark.parametrize("kernel", ["k_epoch_open", "k_epoch_close"])
+@pytest.mark.parametrize("kernel", ["k_epoch_open", "k_epoch_closeE", "k_epoch_close1"])
 def test_flag_accesses_are_scoped_vector_ops(epochs_asm, kernel):
     (lines,) = _kernels(epochs_asm, kernel)
     mem = [l for l in lines if re.match(r"(global|flat|buffer)_(load|store|atomic)", l)]
     assert not [l for l in mem if l.startswith("flat_")]
+    # the one-launch close's arrival count: a 64-bit agent-scope atomic add (as the compiler
+    # lowers it for gfx950)
+    atomics = [l for l in mem if l.startswith("global_atomic")]
+    assert all(l.startswith("global_atomic_add_x2") for l in atomics), atomics
+    mem = [l for l in mem if l not in atomics]
     flags = [l for l in mem if re.match(r"global_(load|store)_dwordx2", l)]
     assert flags
     # 8-B flags and words: host-block flags at system scope, device words at agent scope

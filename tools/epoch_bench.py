@@ -5,7 +5,7 @@ run on two streams of the one GPU, each exchange being ONLY the epoch launches â
 with no data launch in between, so the time per exchange is the protocol's own: the launches,
 the handshake through the host-memory flags, the per-XCD release / acquire fences.
 
-    python tools/epoch_bench.py [K]      -> one JSON line (gpurun_out/ or stdout)
+    python tools/epoch_bench.py [K] [one]   -> one JSON line ("one": the one-launch close)
 
 Reported: us_per_exchange (K back-to-back exchanges per stream, host wall time / K, both streams
 running concurrently), us_per_exchange_graph (the same K exchanges captured into one hipGraph per
@@ -24,6 +24,8 @@ sys.path.insert(0, ROOT)
 
 def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+    one = len(sys.argv) > 2 and sys.argv[2] == "one"  # the one-launch close (phase 2)
+    phases = (2,) if one else (0, 1)
     import torch
     from ghex_amd import _ghx
     _ghx.lib()
@@ -45,8 +47,8 @@ def main():
         for _ in range(k):
             for r in range(2):
                 s = streams[r].cuda_stream
-                _ghx.call("ghx_epochs_enqueue", eps[r], 0, s)
-                _ghx.call("ghx_epochs_enqueue", eps[r], 1, s)
+                for ph in phases:
+                    _ghx.call("ghx_epochs_enqueue", eps[r], ph, s)
 
     exchanges(20)
     torch.cuda.synchronize()
@@ -63,8 +65,8 @@ def main():
             with torch.cuda.graph(g, stream=streams[r]):
                 s = torch.cuda.current_stream().cuda_stream
                 for _ in range(G):
-                    _ghx.call("ghx_epochs_enqueue", eps[r], 0, s)
-                    _ghx.call("ghx_epochs_enqueue", eps[r], 1, s)
+                    for ph in phases:
+                        _ghx.call("ghx_epochs_enqueue", eps[r], ph, s)
         graphs.append(g)
     reps = max(1, K // G)
     for r in range(2):  # the first replay of each (both needed: each waits for the other)
@@ -84,13 +86,15 @@ def main():
         _ghx.call("ghx_epochs_status", eps[r], ctypes.byref(err), ctypes.byref(ep))
         st.append({"error": err.value, "epoch": ep.value})
     n_ex = 20 + K + G * (reps + 1)
-    out = {"tool": "tools/epoch_bench.py", "exchanges": K, "launches_per_exchange": 2,
+    out = {"tool": "tools/epoch_bench.py", "mode": "one-launch close (phase 2)" if one else
+           "open + close (phases 0, 1)", "exchanges": K, "launches_per_exchange": len(phases),
            "us_per_exchange": round(t_eager * 1e6, 2),
            "us_per_exchange_graph": round(t_graph * 1e6, 2),
            "n_xcc": nx.value, "close_grid": fg.value, "status": st,
            "epochs_ok": all(x["error"] == 0 and x["epoch"] == n_ex for x in st),
-           "note": "two ranks (one flag block, two streams, one GPU), each exchange = open + close "
-                   "with no data launch: the protocol's fixed cost incl. the cross-rank handshake"}
+           "note": "two ranks (one flag block, two streams, one GPU), each exchange = the epoch "
+                   "launches with no data launch: the protocol's fixed cost incl. the cross-rank "
+                   "handshake"}
     for h in eps:
         _ghx.call("ghx_epochs_destroy", h)
     print(json.dumps(out), flush=True)

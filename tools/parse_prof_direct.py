@@ -14,7 +14,8 @@ import sys
 
 
 def short(name):
-    for k in ("k_epoch_open", "k_epoch_close", "k_epoch", "k_sys_release", "k_sys_acquire"):
+    for k in ("k_epoch_open", "k_epoch_close1", "k_epoch_close", "k_epoch", "k_sys_release",
+              "k_sys_acquire"):
         if k + "(" in name:
             return k
     if "k_copy<true" in name:
@@ -47,16 +48,18 @@ def main(d):
         kern = {k: {"count": len(v), "avg_us": round(statistics.mean(v), 2),
                     "median_us": round(statistics.median(v), 2),
                     "min_us": round(min(v), 2), "max_us": round(max(v), 2)} for k, v in per.items()}
-        # exchanges: each k_epoch_open starts one; it ends with the next unpack
+        # exchanges: each data pack (k_copy<pack> or the mixed k_self) starts one, preceded by
+        # a k_epoch_open in the two-launch form; it ends with the next unpack
         spans, extra, launches = [], [], []
         i = 0
         while i < len(rows):
-            if rows[i][2] != "k_epoch_open":
+            if rows[i][2] not in ("k_copy<pack>", "k_self"):
                 i += 1
                 continue
-            j = i + 1
+            first = i - 1 if i > 0 and rows[i - 1][2] == "k_epoch_open" else i
+            j = i
             data = 0.0
-            n_ep = 1
+            n_ep = 1 if first < i else 0
             while j < len(rows) and rows[j][2] != "k_copy<unpack>":
                 if rows[j][2].startswith("k_epoch"):
                     n_ep += 1
@@ -66,7 +69,7 @@ def main(d):
             if j == len(rows):
                 break
             data += (rows[j][1] - rows[j][0]) / 1e3
-            span = (rows[j][1] - rows[i][0]) / 1e3
+            span = (rows[j][1] - rows[first][0]) / 1e3
             spans.append(span)
             extra.append(span - data)
             launches.append(n_ep)
