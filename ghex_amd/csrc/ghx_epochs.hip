@@ -1,41 +1,42 @@
 // ghx_epochs.hip — device-side access epochs for the zero-copy exchanges (bulk puts, direct
 // pack): the reference's access guards (include/ghex/rma/access_guard.hpp:35-140,
-// shmem/access_guard.hpp) made stream-ordered, so that an exchange is
-//     k_epoch_open  ->  data launch(es)  ->  k_epoch_close
-// on the caller's stream: two small launches per exchange, no host drain, no global barrier
+// shmem/access_guard.hpp) made stream-ordered:
+//     puts:    k_epoch_open -> put launch(es) -> k_epoch_close      (phases 0, 1)
+//     direct:  pack -> k_epoch_close1 -> unpack                     (phase 2, double buffers)
+// on the caller's stream, with no host drain and no global barrier
 // (include/ghex/bulk_communication_object.hpp:621-694 opens every target range, puts into each
 // source range as soon as it is writable, and waits for its own target ranges to be written).
 //
-// Flag block: one POSIX shared-memory segment per node-local group of ranks (indexed by the rank's
-// position in that group, not its global rank), registered with the GPU (hipHostRegister, mapped:
-// fine-grained, coherent host memory), so every rank's GPU reads and writes every rank's flags
-// over the same physical pages. One flag per 64-B line:
-//   epoch[r]    rank r's exchange counter (written by r only; the host reads it)
-//   error[r]    0, or why r's exchange failed (error codes below; written by r or by its peers)
-//   open[r][t]  = e: target t has opened its halos / receive buffers for r's writes of epoch e
-//   done[r][s]  = e: source s's writes of epoch e into r's memory are complete and visible
-// Device words (this rank's own GPU memory, one per 64-B line): the epoch in flight and whether
-// its open phase failed, one "written back" word per XCD and the leader's "go" word.
+// Where the flags live:
+//   inbox of rank R — fine-grained device memory on R's GPU (coherent across agents), IPC-mapped
+//     into R's node-local peers: open[t] = e (target t opened its memory for R's writes of
+//     epoch e; written by t) and done[s] = e (source s's writes of e into R's memory are complete
+//     and visible; written by s). R polls only its own inbox, locally.
+//   host block — one POSIX shm segment per host, indexed by node-local rank: epoch[r] and
+//     error[r] for the host (ghx_epochs_status), and each rank's inbox IPC handle.
+//   device words of R (plain device memory): the epoch counter and a failure mark, one
+//     "written back" word per XCD, the leader's "go", an arrival count, and R's error word.
 //
-// Exchange on rank R, epoch e = epoch + 1:
-//   open  (one wave): epoch = e; open[s][R] = e for every source s; wait until open[R][t] >= e
-//         for every target t (their memory is writable).
+// Exchange on rank R, epoch e = counter + 1:
+//   open  (one wave): counter = e; open[R] = e in every source's inbox; wait until every target
+//         has written open[t] >= e into R's inbox (their memory is writable).
 //   close (a few one-wave workgroups on EVERY XCD — the XCD count is queried, and the leader
 //         checks that each XCD really ran one):
 //         every workgroup: system-scope release (writes back its XCD's L2: the data launch's
 //           remote writes leave every XCD's L2 for the target's memory) -> "XCD x written back";
-//         leader: once every XCD has written back, done[t][R] = e for every target (with the
-//           FAIL bit when R's own open wait failed), then wait until done[R][s] >= e for every
-//           source -> "go";
+//         leader: once every XCD has written back, done[R] = e in every target's inbox (with the
+//           FAIL bit when R's own open wait failed), then wait until every source's done >= e
+//           -> "go";
 //         every workgroup, after "go": system-scope acquire (invalidates its XCD's L2 and its
 //           CU's L1), so the kernels after the close read what the sources wrote, not stale lines.
+//   close1 (phase 2): see k_epoch_close1.
 // Every rank runs the same number of exchanges, so the epochs agree without any reset; the
 // counters live in memory, so a captured graph replays correctly (every replay a new epoch).
-// Waits are bounded: past the timeout a wave records error[R] and leaves, and the host raises
-// (ghx_epochs_status). A failure reaches both sides: a rank whose open wait timed out (its data
-// launch may have written into a target still reading that memory) marks its done flags FAIL,
-// and every target that sees FAIL records error 4 with the source's index; a wait also ends as
-// soon as someone has recorded an error for this rank.
+// Waits are bounded: past the timeout a wave records R's error and leaves, and the host raises
+// (ghx_epochs_status). A failure reaches both sides: a rank whose wait timed out (its next data
+// launch may write into a target still reading that memory) marks its done flags FAIL, and every
+// target that sees FAIL records error 4 with the source's index; a wait also ends as soon as an
+// error is recorded for this rank.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
@@ -64,27 +65,37 @@ constexpr uint64_t kErrOpen = 1, kErrClose = 2, kErrFence = 3, kErrPeer = 4;  //
 
 struct epoch_args
 {
-    uint64_t* flags;  // device view of the host flag block (8 uint64 per line)
+    uint64_t* flags;  // device view of the host block (status: epoch and error per rank)
     uint64_t* dev;    // this rank's device words (8 uint64 per line)
+    uint64_t* box;    // this rank's inbox (fine-grained device memory, the peers write into it)
     int32_t rank, world;
     int32_t n_src, n_tgt;
     int32_t n_xcc;
     uint64_t timeout_ticks;  // wall-clock ticks (hipDeviceAttributeWallClockRate kHz)
     int16_t src[kMaxPeers], tgt[kMaxPeers];
+    uint64_t* src_box[kMaxPeers];  // the sources' inboxes (IPC mappings; this process's own
+    uint64_t* tgt_box[kMaxPeers];  // when a peer is a thread of it)
 };
 
-// host block: line indices
-__host__ __device__ inline size_t l_epoch(int r, int W) { return 1 + size_t(r) * (2 + 2 * size_t(W)); }
+// host block (one per host, POSIX shm): line 0 = {magic, world}; per rank r: the epoch and the
+// error for the host (ghx_epochs_status), and its inbox's IPC handle (64 B) + {offset, pid, ptr}
+__host__ __device__ inline size_t l_epoch(int r, int W) { return 1 + size_t(r) * 4; }
 __host__ __device__ inline size_t l_error(int r, int W) { return l_epoch(r, W) + 1; }
-__host__ __device__ inline size_t l_open(int r, int t, int W) { return l_epoch(r, W) + 2 + size_t(t); }
-__host__ __device__ inline size_t l_done(int r, int s, int W) { return l_epoch(r, W) + 2 + size_t(W) + size_t(s); }
-inline size_t block_lines(int W) { return 1 + size_t(W) * (2 + 2 * size_t(W)); }
-// device words: line 0 = {epoch counter, failure mark}, 1 + x = XCD x written back, go, and the
-// one-launch close's arrival count
+inline size_t l_handle(int r) { return 1 + size_t(r) * 4 + 2; }
+inline size_t block_lines(int W) { return 1 + size_t(W) * 4; }
+// inbox of rank R (fine-grained device memory on R's GPU; 64-B lines):
+//   open[t] = e: target t has opened its halos / receive buffers for R's writes of epoch e
+//   done[s] = e: source s's writes of epoch e into R's memory are complete and visible
+__host__ __device__ inline size_t in_open(int t) { return size_t(t); }
+__host__ __device__ inline size_t in_done(int s, int W) { return size_t(W) + size_t(s); }
+inline size_t box_lines(int W) { return 2 * size_t(W); }
+// device words: line 0 = {epoch counter, failure mark}, 1 + x = XCD x written back, go, the
+// one-launch close's arrival count, and this rank's error (polled by its own waits)
 constexpr size_t d_rel(int x) { return 1 + size_t(x); }
 constexpr size_t d_go = 1 + kMaxXcc;
 constexpr size_t d_arrive = d_go + 1;
-constexpr size_t kDevLines = d_arrive + 1;
+constexpr size_t d_err = d_arrive + 1;
+constexpr size_t kDevLines = d_err + 1;
 
 __device__ __forceinline__ uint64_t* at(uint64_t* f, size_t line) { return f + line * 8; }
 
@@ -117,15 +128,22 @@ __device__ __forceinline__ unsigned xcc_id()
     return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf;
 }
 
-// One wave: every lane with a flag polls it until it reaches e (flag values may carry kFail);
-// lane 63 polls R's error line. Returns 0 once every flag has arrived, the recorded error as
-// soon as one is set (by R's own earlier wave or by a peer), or `code` after recording it on
-// timeout. *seen: the lane's last flag value (for the FAIL bit).
-__device__ uint64_t wave_wait(uint64_t* err_line, uint64_t* flag, uint64_t e, uint64_t timeout,
-                              uint64_t code, uint64_t* seen)
+// this rank's error: the device word its waits poll, and the host's copy (ghx_epochs_status)
+__device__ __forceinline__ void record(const epoch_args& a, uint64_t code)
+{
+    sys_store(at(a.dev, d_err), code);
+    sys_store(at(a.flags, l_error(a.rank, a.world)), code);
+}
+
+// One wave: every lane with a flag polls it (in this rank's inbox) until it reaches e (flag
+// values may carry kFail); lane 63 polls this rank's error word. Returns 0 once every flag has
+// arrived, the recorded error as soon as one is set, or `code` after recording it on timeout.
+// *seen: the lane's last flag value (for the FAIL bit).
+__device__ uint64_t wave_wait(const epoch_args& a, uint64_t* flag, uint64_t e, uint64_t code,
+                              uint64_t* seen)
 {
     const int lane = int(threadIdx.x);
-    uint64_t* p = lane == 63 ? err_line : flag;
+    uint64_t* p = lane == 63 ? at(a.dev, d_err) : flag;
     const uint64_t t0 = wall_clock64();
     for (;;)
     {
@@ -135,12 +153,12 @@ __device__ uint64_t wave_wait(uint64_t* err_line, uint64_t* flag, uint64_t e, ui
         *seen = v;
         const bool pending = lane != 63 && flag && (v & ~kFail) < e;
         if (!__any(pending)) return 0;
-        if (wall_clock64() - t0 > timeout)
+        if (wall_clock64() - t0 > a.timeout_ticks)
         {
-            if (lane == 63) sys_store(err_line, code);
+            if (lane == 63) record(a, code);
             return code;
         }
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(2);
     }
 }
 
@@ -161,18 +179,16 @@ __global__ __launch_bounds__(64) void k_epoch_open(epoch_args a)
 {
     const int lane = int(threadIdx.x);
     const int R = a.rank, W = a.world;
-    uint64_t* f = a.flags;
     const uint64_t e = dev_load(at(a.dev, 0)) + 1;
     if (lane == 0)
     {
         dev_store(at(a.dev, 0), e);
-        sys_store(at(f, l_epoch(R, W)), e);  // the host's view (ghx_epochs_status)
+        sys_store(at(a.flags, l_epoch(R, W)), e);  // the host's view (ghx_epochs_status)
     }
-    if (lane < a.n_src) sys_store(at(f, l_open(a.src[lane], R, W)), e);  // halos / buffers open
+    if (lane < a.n_src) sys_store(at(a.src_box[lane], in_open(R)), e);  // halos / buffers open
     uint64_t seen;
-    const uint64_t err = wave_wait(at(f, l_error(R, W)),
-                                   lane < a.n_tgt ? at(f, l_open(R, a.tgt[lane], W)) : nullptr, e,
-                                   a.timeout_ticks, kErrOpen, &seen);
+    const uint64_t err = wave_wait(a, lane < a.n_tgt ? at(a.box, in_open(a.tgt[lane])) : nullptr,
+                                   e, kErrOpen, &seen);
     // a failed open phase makes this epoch's done flags FAIL (the data launch runs anyway: its
     // writes may have hit memory a target was still reading, and the target must know)
     if (err && lane == 0) dev_store(at(a.dev, 0) + 1, e);
@@ -184,7 +200,6 @@ __global__ __launch_bounds__(64) void k_epoch_close(epoch_args a)
 {
     const int lane = int(threadIdx.x);
     const int R = a.rank, W = a.world;
-    uint64_t* f = a.flags;
     uint64_t* dv = a.dev;
     // the data launch's writes into the targets' memory leave this XCD's L2: the write-back is
     // issued first and overlaps the loads of the epoch words; the explicit wait covers both
@@ -202,20 +217,18 @@ __global__ __launch_bounds__(64) void k_epoch_close(epoch_args a)
             !wave_wait_dev(lane < a.n_xcc ? at(dv, d_rel(lane)) : nullptr, e, a.timeout_ticks))
         {
             err = kErrFence;
-            if (lane == 0) sys_store(at(f, l_error(R, W)), kErrFence);
+            if (lane == 0) record(a, kErrFence);
         }
         const uint64_t mark = (open_failed || err) ? kFail : 0;
-        if (lane < a.n_tgt) sys_store(at(f, l_done(a.tgt[lane], R, W)), e | mark);
+        if (lane < a.n_tgt) sys_store(at(a.tgt_box[lane], in_done(R, W)), e | mark);
         if (!err)
         {
-            err = wave_wait(at(f, l_error(R, W)),
-                            lane < a.n_src ? at(f, l_done(R, a.src[lane], W)) : nullptr, e,
-                            a.timeout_ticks, kErrClose, &seen);
+            err = wave_wait(a, lane < a.n_src ? at(a.box, in_done(a.src[lane], W)) : nullptr, e,
+                            kErrClose, &seen);
             // a source whose open failed: its writes may have overlapped this rank's last reads
             const bool bad = !err && lane < a.n_src && lane != 63 && (seen & kFail);
             const uint64_t m = __ballot(bad);
-            if (m && lane == int(__builtin_ctzll(m)))
-                sys_store(at(f, l_error(R, W)), kErrPeer | (uint64_t(a.src[lane]) << 8));
+            if (m && lane == int(__builtin_ctzll(m))) record(a, kErrPeer | (uint64_t(a.src[lane]) << 8));
         }
         if (lane == 0 && a.n_src > 0) dev_store(at(dv, d_go), e);
     }
@@ -224,7 +237,7 @@ __global__ __launch_bounds__(64) void k_epoch_close(epoch_args a)
         // the leader sets go within its own bounded waits (2 x timeout at most): a follower
         // that outlasts 3 x timeout means the leader never ran
         if (!wave_wait_dev(lane == 0 ? at(dv, d_go) : nullptr, e, 3 * a.timeout_ticks) && lane == 0)
-            sys_store(at(f, l_error(R, W)), kErrFence);
+            record(a, kErrFence);
     }
     // what the sources wrote is read by the kernels after this one: no stale line in this XCD's
     // L2 (nor this CU's L1; the next launch invalidates the other CUs' L1s). A rank without
@@ -236,18 +249,18 @@ __global__ __launch_bounds__(64) void k_epoch_close(epoch_args a)
 // before it wrote copy e&1 of each target's buffers, the unpack after it reads copy e&1 of this
 // rank's. No open phase: the copy a source writes at e+1 was last read by this rank's unpack of
 // e-1, which ran before this close (stream order), so this close tells its sources so
-// (open[s][R] = e) together with done[t][R] = e, and waits for both from its peers:
+// (open[R] = e in their inboxes) together with done[R] = e in its targets', and waits for both
+// from its peers:
 //   every workgroup: system-scope release (if it has targets) -> "XCD x written back"; arrive;
 //   leader: every XCD written back and every workgroup arrived (all have read the counter);
-//     done[t][R] = e (FAIL after an earlier failure of R) and open[s][R] = e; wait until
-//     done[R][s] >= e (the sources' writes of e are in copy e&1) and open[R][t] >= e (the
-//     targets are done reading the copy R writes at e+1); counter = e; go;
+//     done and open flags (done with FAIL after an earlier failure of R); wait until every
+//     source's done >= e (its writes of e are in copy e&1) and every target's open >= e (it is
+//     done reading the copy R writes at e+1); counter = e; go;
 //   every workgroup after go: system-scope acquire.
 __global__ __launch_bounds__(64) void k_epoch_close1(epoch_args a)
 {
     const int lane = int(threadIdx.x);
     const int R = a.rank, W = a.world;
-    uint64_t* f = a.flags;
     uint64_t* dv = a.dev;
     if (a.n_tgt > 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
     const uint64_t e = dev_load(at(dv, 0)) + 1;
@@ -266,32 +279,31 @@ __global__ __launch_bounds__(64) void k_epoch_close1(epoch_args a)
             err = kErrFence;
         if (!err && !wave_wait_dev(lane == 0 ? at(dv, d_arrive) : nullptr, e * gridDim.x, a.timeout_ticks))
             err = kErrFence;
-        if (err && lane == 0) sys_store(at(f, l_error(R, W)), err);
+        if (err && lane == 0) record(a, err);
         const uint64_t mark = (failed_before || err) ? kFail : 0;
-        if (lane < a.n_tgt) sys_store(at(f, l_done(a.tgt[lane], R, W)), e | mark);
-        if (lane < a.n_src) sys_store(at(f, l_open(a.src[lane], R, W)), e);
+        if (lane < a.n_tgt) sys_store(at(a.tgt_box[lane], in_done(R, W)), e | mark);
+        if (lane < a.n_src) sys_store(at(a.src_box[lane], in_open(R)), e);
         if (!err)
         {
             // lanes [0, n_src): the sources' done flags; [n_src, n_src + n_tgt): the targets'
             const int ns = a.n_src, nt = a.n_tgt;
-            uint64_t* flag = lane < ns ? at(f, l_done(R, a.src[lane], W))
-                             : lane < ns + nt ? at(f, l_open(R, a.tgt[lane - ns], W)) : nullptr;
-            err = wave_wait(at(f, l_error(R, W)), flag, e, a.timeout_ticks, kErrClose, &seen);
+            uint64_t* flag = lane < ns ? at(a.box, in_done(a.src[lane], W))
+                             : lane < ns + nt ? at(a.box, in_open(a.tgt[lane - ns])) : nullptr;
+            err = wave_wait(a, flag, e, kErrClose, &seen);
             const bool bad = !err && lane < ns && (seen & kFail);
             const uint64_t m = __ballot(bad);
-            if (m && lane == int(__builtin_ctzll(m)))
-                sys_store(at(f, l_error(R, W)), kErrPeer | (uint64_t(a.src[lane]) << 8));
+            if (m && lane == int(__builtin_ctzll(m))) record(a, kErrPeer | (uint64_t(a.src[lane]) << 8));
         }
         if (lane == 0)
         {
             if (err) dev_store(at(dv, 0) + 1, 1);  // later done flags carry FAIL
             dev_store(at(dv, 0), e);
             dev_store(at(dv, d_go), e);
-            sys_store(at(f, l_epoch(R, W)), e);  // the host's view (ghx_epochs_status)
+            sys_store(at(a.flags, l_epoch(R, W)), e);  // the host's view (ghx_epochs_status)
         }
     }
     else if (!wave_wait_dev(lane == 0 ? at(dv, d_go) : nullptr, e, 4 * a.timeout_ticks) && lane == 0)
-        sys_store(at(f, l_error(R, W)), kErrFence);  // the leader never ran (its waits are bounded)
+        record(a, kErrFence);  // the leader never ran (its waits are bounded)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
 }
 }  // namespace
@@ -306,14 +318,41 @@ struct ghx_epochs
     size_t bytes = 0;
     bool registered = false;
     uint64_t* dev = nullptr;
+    uint64_t* box = nullptr;                 // this rank's inbox (fine-grained device memory)
+    std::vector<std::pair<int, void*>> imports;  // (node-local rank, IPC mapping of its inbox)
     int fence_groups = 0;
     int mode = -1;  // 0: open + close (phases 0, 1); 1: one-launch close (phase 2)
     epoch_args args{};
+    void close_imports()
+    {
+        for (auto& kv : imports)
+            if (kv.second) (void)hipIpcCloseMemHandle(kv.second);
+        imports.clear();
+    }
     ~ghx_epochs()
     {
+        close_imports();
+        if (box) (void)hipFree(box);
         if (dev) (void)hipFree(dev);
         if (registered) (void)hipHostUnregister(host);
         if (host) munmap(host, bytes);
+    }
+    // rank r's inbox in this process: its IPC mapping (or the pointer itself when r is this
+    // process, e.g. two ranks as threads of one process)
+    uint64_t* inbox_of(int r)
+    {
+        for (auto& kv : imports)
+            if (kv.first == r) return static_cast<uint64_t*>(kv.second);
+        const volatile uint64_t* meta = line(l_handle(r) + 1);
+        if (meta[3] != kMagic) throw invalid("a peer has not published its epoch inbox (not attached?)");
+        if (int64_t(meta[1]) == int64_t(getpid())) return reinterpret_cast<uint64_t*>(meta[2]);
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, const_cast<const uint64_t*>(line(l_handle(r))), sizeof(h));
+        void* p = nullptr;
+        if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+            throw hip_error("hipIpcOpenMemHandle(a peer's epoch inbox)");
+        imports.emplace_back(r, p);
+        return static_cast<uint64_t*>(p) + meta[0] / sizeof(uint64_t);
     }
     volatile uint64_t* line(size_t l) const { return static_cast<volatile uint64_t*>(host) + l * 8; }
 };
@@ -388,11 +427,27 @@ int ghx_epochs_create(const char* name, int32_t create, int32_t world, int32_t r
             xcc > kMaxXcc)
             throw hip_error("hipDeviceGetAttribute(number of XCCs) gave no usable count");
         if (hipMalloc(&ep->dev, kDevLines * 64) != hipSuccess) throw hip_error("hipMalloc(epoch words)");
-        if (hipMemset(ep->dev, 0, kDevLines * 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        // the inbox the peers write their flags into: fine-grained device memory (coherent across
+        // agents, polled locally), published to the host's other ranks through the host block
+        if (hipExtMallocWithFlags(reinterpret_cast<void**>(&ep->box), box_lines(world) * 64,
+                                  hipDeviceMallocFinegrained) != hipSuccess)
+            throw hip_error("hipExtMallocWithFlags(epoch inbox, fine-grained)");
+        if (hipMemset(ep->dev, 0, kDevLines * 64) != hipSuccess ||
+            hipMemset(ep->box, 0, box_lines(world) * 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
             throw hip_error("hipMemset(epoch words)");
+        hipIpcMemHandle_t h;
+        if (hipIpcGetMemHandle(&h, ep->box) != hipSuccess) throw hip_error("hipIpcGetMemHandle(epoch inbox)");
+        static_assert(sizeof(h) <= 64, "IPC handle fits a line");
+        std::memcpy(const_cast<uint64_t*>(ep->line(l_handle(rank))), &h, sizeof(h));
+        volatile uint64_t* meta = ep->line(l_handle(rank) + 1);
+        meta[0] = 0;  // offset of the inbox in its allocation
+        meta[1] = uint64_t(getpid());
+        meta[2] = reinterpret_cast<uint64_t>(ep->box);
+        meta[3] = kMagic;  // published last
         ep->fence_groups = kFencePerXcc * xcc;
         ep->args.flags = static_cast<uint64_t*>(dptr);
         ep->args.dev = ep->dev;
+        ep->args.box = ep->box;
         ep->args.rank = rank;
         ep->args.world = world;
         ep->args.n_xcc = xcc;
@@ -426,6 +481,11 @@ int ghx_epochs_peers(ghx_epochs* ep, const int32_t* sources, int32_t n_sources,
             if (r < 0 || r >= ep->args.world || r == ep->args.rank)
                 throw invalid("peer out of range of the node-local group (or this rank itself)");
         }
+        // the peers' inboxes (every peer has attached: the caller's setup passed its barrier)
+        ep->close_imports();
+        ep->args.n_src = ep->args.n_tgt = 0;
+        for (int i = 0; i < n_sources; ++i) ep->args.src_box[i] = ep->inbox_of(sources[i]);
+        for (int i = 0; i < n_targets; ++i) ep->args.tgt_box[i] = ep->inbox_of(targets[i]);
         ep->args.n_src = n_sources;
         ep->args.n_tgt = n_targets;
         for (int i = 0; i < n_sources; ++i) ep->args.src[i] = int16_t(sources[i]);

@@ -10,7 +10,7 @@ GPUs over xGMI on a multi-GPU node). Modes "direct*": the CommunicationObject's 
 (the pack writes into the receivers' buffers through IPC mappings; device epochs). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directrace|directgraph|udirect]
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directloop|directrace|directgraph|udirect|slowdirect|slowbulk]
 (udirect: <px> <py> <pz> = world split, <N> = cells per rank, <H> = levels)"""
 import os
 import sys
@@ -112,13 +112,21 @@ def main():
             co.check_epochs()
             bad += int(nbad.item())
             continue
-        elif mode in ("direct", "directrace", "directgraph"):
+        elif mode in ("direct", "directloop", "directrace", "directgraph"):
             # the pack writes every peer message straight into the receiver's buffer (IPC),
             # device epochs order it; the receiver unpacks locally (no transport step)
             co = R.make_communication_object(ctx, direct=True, epoch_timeout=60)
             if mode == "direct":
                 for _ in range(reps):
                     co.exchange([pc(fd)]).wait()
+            elif mode == "directloop":
+                # back to back on the stream, one host wait at the end: the ranks' devices stay
+                # in step through the epochs alone (tools/prof_direct.sh traces this)
+                co.exchange([pc(fd)]).wait()
+                for _ in range(reps):
+                    co.exchange([pc(fd)])
+                    co._valid = False
+                co.exchange([pc(fd)]).wait()
             else:
                 # rewrite / exchange / check on the stream with no host synchronisation (race),
                 # or the exchange captured once into a graph and replayed (graph): a pack that

@@ -10,8 +10,9 @@ for the epoch kernels (ghex_amd/csrc/ghx_epochs.hip) and for the kernels that wr
   publishes "this XCD is written back", and ends in a system-scope acquire (`buffer_inv sc0 sc1`)
   behind a wait (ranks with sources; nothing touches memory after it); the open kernel, whose
   flags follow reads only, has no fence;
-* every flag access in host memory is a system-scope vector access (`sc0 sc1`), every device
-  word an agent-scope one (`sc1`), none through `flat_` instructions;
+* every flag access (the inboxes in fine-grained device memory, the host block) is a
+  system-scope vector access (`sc0 sc1`), every device word an agent-scope one (`sc1`), none
+  through `flat_` instructions;
 * the peer-writing kernels store through `global_store_*` (no `flat_`, no non-temporal stores
   whose write-back the release would not cover).
 Reference: include/ghex/rma/cuda/handle.hpp:20-96 (the CUDA IPC path these replace)."""
@@ -118,14 +119,18 @@ def test_flag_accesses_are_scoped_vector_ops(epochs_asm, kernel):
     atomics = [l for l in mem if l.startswith("global_atomic")]
     assert all(l.startswith("global_atomic_add_x2") for l in atomics), atomics
     mem = [l for l in mem if l not in atomics]
-    flags = [l for l in mem if re.match(r"global_(load|store)_dwordx2", l)]
-    assert flags
-    # 8-B flags and words: host-block flags at system scope, device words at agent scope
-    assert all(l.endswith(" sc1") for l in flags), [l for l in flags if not l.endswith(" sc1")]
-    assert any(l.endswith(" sc0 sc1") and "store" in l for l in flags)
-    assert any(l.endswith(" sc0 sc1") and "load" in l for l in flags)
-    # the only other loads: the peer lists from the kernel arguments (read-only)
-    assert all(re.match(r"global_load_ushort", l) for l in mem if l not in flags)
+    # every store is a flag or word store, at system (`sc0 sc1`) or agent (`sc1`) scope
+    stores = [l for l in mem if "_store" in l]
+    assert stores and all(l.endswith(" sc1") for l in stores), [l for l in stores if not l.endswith(" sc1")]
+    # every load either polls a flag or word (`sc1` / `sc0 sc1`) or reads the kernel arguments
+    # (the peer lists and the peers' inbox pointers: plain loads of the read-only kernarg
+    # segment, 16-bit ranks and 64-bit pointers)
+    loads = [l for l in mem if "_load" in l]
+    polls = [l for l in loads if l.endswith(" sc1")]
+    plain = [l for l in loads if l not in polls]
+    assert any(l.endswith(" sc0 sc1") for l in polls) and any(l.endswith(" sc1") for l in polls)
+    assert all(re.match(r"global_load_(ushort|dwordx2) ", l) and " sc" not in l for l in plain), plain
+    assert any(l.endswith(" sc0 sc1") for l in stores)
 
 
 @pytest.fixture(scope="module")

@@ -65,7 +65,7 @@ _CASES = [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)]
                          [(_CASES[0][0], _CASES[0][1], _CASES[0][2], "bulkmixed")] +
                          [(c[0], c[1], c[2], "direct") for c in _CASES] +
                          [(_CASES[1][0], _CASES[1][1], _CASES[1][2], m)
-                          for m in ("directrace", "directgraph")])
+                          for m in ("directrace", "directgraph", "directloop")])
 def test_exchange_multi_process(parts, N, Hw, mode):
     """staged: CommunicationObject(staging="host") over gloo; bulk: zero-copy IPC puts ordered by
     device-side epochs (bulkhost: by host drains + barriers; bulkrace: device epochs as the only

@@ -4,7 +4,7 @@ exchange; and per exchange (open start -> unpack end on the rank's stream) the s
 minus the pack and unpack kernels (what the epochs add: their launches, fences and the wait for
 the peer, which shares the GPU here).
 
-usage: python tools/parse_prof_direct.py gpurun_out/prof_direct > profiles/r04_direct_kernel_trace.json"""
+usage: python tools/parse_prof_direct.py gpurun_out/prof_direct [worker mode, default directloop]"""
 import csv
 import glob
 import json
@@ -27,9 +27,11 @@ def short(name):
     return name[:60]
 
 
-def main(d):
+def main(d, mode="directloop"):
+    how = ("back to back on the stream" if mode == "directloop" else
+           "each awaited on the host")
     out = {"source": "tools/prof_direct.sh: rocprofv3 --kernel-trace of tests/mp_exchange_worker.py "
-                     "2 1 1 128 2 40 direct (two field layouts, 40 exchanges each after one setup), "
+                     f"2 1 1 128 2 40 {mode} (two field layouts, 40 exchanges each, {how}), "
                      "2 processes sharing one MI355X: a close kernel's duration includes its wait "
                      "for the peer's pack", "ranks": {}}
     for r in (0, 1):
@@ -84,4 +86,5 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_direct")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_direct",
+         sys.argv[2] if len(sys.argv) > 2 else "directloop")
