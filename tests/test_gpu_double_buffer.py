@@ -27,7 +27,7 @@ def _dbl(n):
     return max(256, (n + 255) // 256 * 256)
 
 
-def _ranks(parts, N, Hw):
+def _ranks(parts, N, Hw, nf=1):
     import torch
     from ghex_amd.structured import regular as R
     from tests.gpu_util import FakeContext, device_field
@@ -40,12 +40,16 @@ def _ranks(parts, N, Hw):
         dom = ranks[r][0]
         dd = R.DomainDescriptor(dom.id, dom.first, dom.last)
         pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (1, 1, 1)), [dd])
-        a, _ = H.linear_index_field(dom, N, Hw, gl)
-        exp = H.expected_linear_halo(a, dom, N, Hw, gl)
-        base, logical = device_field(a, (2, 1, 0))
-        fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)
-        out.append(dict(co=R.make_communication_object(ctx), bis=[pc(fd)], base=base, a=a,
-                        exp=exp, rank=r))
+        bis, bases, arrs, exps = [], [], [], []
+        for k in range(nf):  # field k = linear index + k
+            a, _ = H.linear_index_field(dom, N, Hw, gl, add=k)
+            base, logical = device_field(a, (2, 1, 0))
+            bis.append(pc(R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)))
+            bases.append(base)
+            arrs.append(a)
+            exps.append(H.expected_linear_halo(a, dom, N, Hw, gl) + k)
+        out.append(dict(co=R.make_communication_object(ctx), bis=bis, bases=bases, arrs=arrs,
+                        exps=exps, rank=r))
     torch.cuda.synchronize()
     return out
 
@@ -57,18 +61,21 @@ def _set(plan, direction, word, add, offsets):
               (ctypes.c_int64 * max(1, len(offsets)))(*offsets), len(offsets))
 
 
-@pytest.mark.parametrize("parts,N,Hw", [((2, 1, 1), 12, 2), ((2, 2, 1), 9, 1), ((1, 1, 2), 10, 3)])
+@pytest.mark.parametrize("parts,N,Hw,nf", [((2, 1, 1), 12, 2, 1), ((2, 2, 1), 9, 1, 1),
+                                           ((1, 1, 2), 10, 3, 1), ((2, 1, 1), 6, 1, 70)])
 @pytest.mark.parametrize("mixed", [False, True])
 @pytest.mark.parametrize("graph", [False, True])
-def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, mixed, graph):
+def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, nf, mixed, graph):
     """Each rank's send buffers and peer receive buffers exist twice (the odd copy at
-    _dbl(size)); every exchange k sets the device word to k, packs with add 1 (copy (k+1)&1) and
-    unpacks with add 0 (copy k&1) after routing the packed copy into the receiver's copy of the
-    same parity. Every packed byte must land in the selected copy only, and every cell must come
-    out right — with the launches eager, or captured once and replayed."""
+    _dbl(size)). Exchange k packs with the device word at k - 1 and add 1, as before the epoch
+    close, then unpacks with the word at k and add 0, as after it: both select copy k&1, and the
+    test routes the packed copy into the receiver's copy of the same parity in between. Every
+    packed byte must land in the selected copy only, and every cell must come out right — with
+    the launches eager, or captured once and replayed; 70 fields cut the plans into launch
+    groups (each with its own slot map of the copies' offsets)."""
     import torch
     from ghex_amd import _ghx
-    rs = _ranks(parts, N, Hw)
+    rs = _ranks(parts, N, Hw, nf)
     L = _ghx.lib()
     word = torch.zeros(1, dtype=torch.int64, device="cuda")
     st = []
@@ -90,7 +97,7 @@ def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, mixed, graph):
         roff = [_dbl(b["size"]) if b["rank"] != me else 0 for b in plan.recv]
         _set(plan, 0, word, 1, soff)
         _set(plan, 1, word, 0, roff)
-        f = _ghx.ptr_array([bis[0].field.data_ptr()])
+        f = _ghx.ptr_array([bi.field.data_ptr() for bi in bis])
         st.append(dict(x, plan=plan, send=send, recv=recv, soff=soff, roff=roff, f=f, mixed=m,
                        sp=_ghx.ptr_array([t.data_ptr() for t in send]),
                        rp=_ghx.ptr_array([t.data_ptr() for t in recv])))
@@ -98,12 +105,12 @@ def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, mixed, graph):
     def pack(s):
         for x in st:
             fn = L.ghx_exchange_pack_self if x["mixed"] else L.ghx_exchange_pack
-            _ghx.check(fn(x["plan"].h, x["f"], 1, x["sp"], len(x["send"]), s), "pack")
+            _ghx.check(fn(x["plan"].h, x["f"], len(x["bis"]), x["sp"], len(x["send"]), s), "pack")
 
     def unpack(s):
         for x in st:
             fn = L.ghx_exchange_unpack_peers if x["mixed"] else L.ghx_exchange_unpack
-            _ghx.check(fn(x["plan"].h, x["f"], 1, x["rp"], len(x["recv"]), s), "unpack")
+            _ghx.check(fn(x["plan"].h, x["f"], len(x["bis"]), x["rp"], len(x["recv"]), s), "unpack")
 
     def route(k):
         """the transport: each peer message's copy k&1 into the receiver's copy k&1"""
@@ -133,7 +140,8 @@ def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, mixed, graph):
             unpack(torch.cuda.current_stream().cuda_stream)
     for k in (1, 2, 3, 4):
         for x in st:  # reset the halos and both copies of every buffer
-            x["base"].copy_(torch.from_numpy(x["a"]).cuda())
+            for base, a in zip(x["bases"], x["arrs"]):
+                base.copy_(torch.from_numpy(a).cuda())
             for t in x["send"] + x["recv"]:
                 t.fill_(255)
         word.fill_(k - 1)  # the pack of exchange k reads k - 1 (+1): copy k&1
@@ -153,7 +161,8 @@ def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, mixed, graph):
         gu.replay() if graph else unpack(s)
         torch.cuda.synchronize()
         for x in st:
-            assert np.array_equal(x["base"].cpu().numpy(), x["exp"]), (k, x["rank"])
+            for f, (base, exp) in enumerate(zip(x["bases"], x["exps"])):
+                assert np.array_equal(base.cpu().numpy(), exp), (k, x["rank"], f)
     for x in st:  # back to single buffers
         _set(x["plan"], 0, None, 0, [])
         _set(x["plan"], 1, None, 0, [])
