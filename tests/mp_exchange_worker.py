@@ -10,7 +10,7 @@ GPUs over xGMI on a multi-GPU node). Modes "direct*": the CommunicationObject's 
 (the pack writes into the receivers' buffers through IPC mappings; device epochs). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directloop|directrace|directgraph|udirect|slowdirect|slowbulk]
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directloop|directrace|directgraph|directmany|udirect|slowdirect|slowbulk]
 (udirect: <px> <py> <pz> = world split, <N> = cells per rank, <H> = levels)"""
 import os
 import sys
@@ -108,6 +108,30 @@ def main():
                 base.copy_(src * f)
                 g.replay()
                 nbad += (base != exp_d * f).sum()
+            torch.cuda.synchronize()
+            co.check_epochs()
+            bad += int(nbad.item())
+            continue
+        elif mode == "directmany":
+            # 70 fields in one direct exchange: the plans split into launch groups, each with
+            # its own slot map of the receive buffers' second copies; rewritten, exchanged and
+            # checked on the stream with no host synchronisation
+            co = R.make_communication_object(ctx, direct=True, epoch_timeout=60)
+            srcs = [torch.from_numpy(a).cuda() + k for k in range(70)]
+            views = [device_field(a + k, layout) for k in range(70)]
+            bases = [b for b, _ in views]
+            bis = [pc(R.make_field_descriptor(dd, v, (Hw,) * 3, (N + 2 * Hw,) * 3))
+                   for _, v in views]
+            exp_d = torch.from_numpy(expect).cuda()
+            nbad = torch.zeros((), dtype=torch.int64, device="cuda")
+            for k in range(2 * reps):
+                f = float(k % 5 + 1)
+                for b, s in zip(bases, srcs):
+                    b.copy_(s * f)
+                co.exchange(bis)
+                co._valid = False
+                for j, b in enumerate(bases):
+                    nbad += (b != (exp_d + j) * f).sum()
             torch.cuda.synchronize()
             co.check_epochs()
             bad += int(nbad.item())

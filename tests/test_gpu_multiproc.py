@@ -62,6 +62,7 @@ _CASES = [((2, 1, 1), 16, 2), ((2, 2, 1), 12, 3), ((1, 1, 2), 9, 1)]
                          [(_CASES[1][0], _CASES[1][1], _CASES[1][2], m)
                           for m in ("stagedrt", "bulkhost", "bulkmixed", "bulkrace", "bulkgraph",
                                     "pipert")] +
+                         [((2, 1, 1), 6, 1, "directmany")] +
                          [(_CASES[0][0], _CASES[0][1], _CASES[0][2], "bulkmixed")] +
                          [(c[0], c[1], c[2], "direct") for c in _CASES] +
                          [(_CASES[1][0], _CASES[1][1], _CASES[1][2], m)
@@ -74,7 +75,8 @@ def test_exchange_multi_process(parts, N, Hw, mode):
     hosts, puts inside a host and a host-staged buffered exchange between them); pipe: the
     pipelined host-staged exchange (per-peer streams, send as each copy lands); direct: the pack
     writes into the receivers' buffers through IPC, device epochs, local unpack (directrace /
-    directgraph: ordered on the stream only / replayed from a graph). Host copies on
+    directgraph: ordered on the stream only / replayed from a graph; directmany: 70 fields, so
+    the plans split into launch groups). Host copies on
     the measured SDMA engines (ghex_amd.staging) by default; stagedrt / pipert: hipMemcpyAsync."""
     _run(parts, N, Hw, mode)
 
