@@ -509,7 +509,8 @@ int ghx_epochs_enqueue(ghx_epochs* ep, int32_t phase, ghx_stream stream)
             throw invalid("the one-launch close waits on at most 63 sources + targets");
         ep->mode = mode;
         const auto s = static_cast<hipStream_t>(stream);
-        if (phase == 1 && ep->args.n_src == 0 && ep->args.n_tgt == 0) return GHX_OK;  // no peers
+        // no peers: nothing to close (and no double-buffered peer message reads the counter)
+        if (phase != 0 && ep->args.n_src == 0 && ep->args.n_tgt == 0) return GHX_OK;
         if (phase == 0)
             hipLaunchKernelGGL(k_epoch_open, dim3(1), dim3(64), 0, s, ep->args);
         else if (phase == 1)

@@ -470,7 +470,8 @@ int ghx_epochs_info(const ghx_epochs* ep, int32_t* n_xcc, int32_t* fence_groups)
  * (ghx_exchange_set_parity with the word ghx_epochs_counter returns): data launch (copy e&1 of
  * the targets') -> ghx_epochs_enqueue(ep, 2, stream) -> unpack (copy e&1 of this rank's). The
  * close tells the sources that this rank's previous unpack is done, which is what the open
- * phase is for otherwise. An object runs phases 0/1 or phase 2, not both. */
+ * phase is for otherwise. An object runs phases 0/1 or phase 2, not both. Without peers the
+ * close phases enqueue nothing. */
 int ghx_epochs_counter(const ghx_epochs* ep, const uint64_t** word);
 int ghx_epochs_destroy(ghx_epochs* ep);
 
