@@ -10,13 +10,30 @@ GPUs over xGMI on a multi-GPU node). Modes "direct*": the CommunicationObject's 
 (the pack writes into the receivers' buffers through IPC mappings; device epochs). Mode "pipe" is the pipelined host-staged exchange (one
 stream per peer: pack, D2H, send as soon as that copy landed, H2D + unpack per arrived message).
 
-usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directloop|directrace|directgraph|directmany|udirect|slowdirect|slowbulk]
+usage: python tests/mp_exchange_worker.py <px> <py> <pz> <N> <H> [n_exchanges] [staged|stagedrt|bulk|bulkhost|bulkmixed|bulkrace|bulkgraph|sched|pipe|pipert|direct|directloop|directrace|directgraph|directnoepoch|directmany|udirect|slowdirect|slowbulk]
 (udirect: <px> <py> <pz> = world split, <N> = cells per rank, <H> = levels)"""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def make_jitter(rank):
+    """GHX_SOAK_JITTER=1 (tools/epoch_soak.py): before each exchange of the race / graph loops a
+    rank queues 0-3 busy kernels (seeded per rank), so the ranks' streams drift apart and the
+    epochs alone keep them in step. Otherwise a no-op."""
+    if os.environ.get("GHX_SOAK_JITTER") != "1":
+        return lambda: None
+    import random
+    import torch
+    rng = random.Random(1000 + rank)
+    scratch = torch.ones(1 << 25, device="cuda")  # 128 MiB: tens of microseconds per kernel
+
+    def jitter():
+        for _ in range(rng.randrange(4)):
+            scratch.mul_(1.0)
+    return jitter
 
 
 def main():
@@ -35,6 +52,7 @@ def main():
     from tests import helpers as H
     from tests.gpu_util import device_field
     ghex_amd.native_library()
+    jitter = make_jitter(rank)
     if mode == "udirect":
         sys.exit(unstructured_direct(rank, world, N, Hw, reps))
     if mode in ("slowdirect", "slowbulk"):
@@ -81,6 +99,7 @@ def main():
             for k in range(4 * reps):
                 f = float(k % 5 + 1)
                 base.copy_(src * f)
+                jitter()
                 h = co.exchange()
                 nbad += (base != exp_d * f).sum()
             h.wait()
@@ -106,6 +125,7 @@ def main():
             for k in range(3 * reps):
                 f = float(k % 5 + 1)
                 base.copy_(src * f)
+                jitter()
                 g.replay()
                 nbad += (base != exp_d * f).sum()
             torch.cuda.synchronize()
@@ -128,6 +148,7 @@ def main():
                 f = float(k % 5 + 1)
                 for b, s in zip(bases, srcs):
                     b.copy_(s * f)
+                jitter()
                 co.exchange(bis)
                 co._valid = False
                 for j, b in enumerate(bases):
@@ -136,7 +157,7 @@ def main():
             co.check_epochs()
             bad += int(nbad.item())
             continue
-        elif mode in ("direct", "directloop", "directrace", "directgraph"):
+        elif mode in ("direct", "directloop", "directrace", "directgraph", "directnoepoch"):
             # the pack writes every peer message straight into the receiver's buffer (IPC),
             # device epochs order it; the receiver unpacks locally (no transport step)
             co = R.make_communication_object(ctx, direct=True, epoch_timeout=60)
@@ -160,6 +181,12 @@ def main():
                 exp_d = torch.from_numpy(expect).cuda()
                 co.exchange([pc(fd)]).wait()
                 run = lambda: co.exchange([pc(fd)])
+                if mode == "directnoepoch":
+                    # negative control of the soak (tools/epoch_soak.py): the same loop with the
+                    # epoch launch left out, so nothing orders the ranks' packs and unpacks; the
+                    # check must see values of other exchanges
+                    for d in co._direct.values():
+                        d["ep_saved"], d["ep"] = d["ep"], None
                 if mode == "directgraph":
                     g = torch.cuda.CUDAGraph()
                     side = torch.cuda.Stream()
@@ -176,10 +203,15 @@ def main():
                 for k in range(4 * reps):
                     f = float(k % 5 + 1)
                     base.copy_(src * f)
+                    jitter()
                     run()
                     co._valid = False  # the next exchange is ordered on the stream, not awaited
                     nbad += (base != exp_d * f).sum()
                 torch.cuda.synchronize()
+                for d in co._direct.values():
+                    if "ep_saved" in d:
+                        d["ep"] = d.pop("ep_saved")
+                dist.barrier()
                 co.check_epochs()
                 bad += int(nbad.item())
                 continue

@@ -27,16 +27,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(parts, N, Hw, mode):
+def _run(parts, N, Hw, mode, reps=3, jitter=False, expect_bad=False):
     world = parts[0] * parts[1] * parts[2]
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), LOCAL_RANK="0")
+                   MASTER_PORT=str(port), LOCAL_RANK="0", GHX_SOAK_JITTER="1" if jitter else "0")
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(HERE, "mp_exchange_worker.py"),
-             *map(str, parts), str(N), str(Hw), "3", mode],
+             *map(str, parts), str(N), str(Hw), str(reps), mode],
             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs, codes = [], []
     for p in procs:
@@ -48,6 +48,9 @@ def _run(parts, N, Hw, mode):
             raise
         outs.append(out)
         codes.append(p.returncode)
+    if expect_bad:
+        assert "bad cells " in outs[0] and "bad cells 0" not in outs[0], "\n".join(outs)
+        return
     assert codes == [0] * world, "\n".join(outs)
     assert "bad cells 0" in outs[0]
 
@@ -105,3 +108,17 @@ def test_epoch_failure_reaches_both_sides(mode):
     wait() raises; the late receiver, whose own waits pass, raises too (the sender marked its
     done flag FAIL: its writes may have overlapped the receiver's reads) — ADVICE r03."""
     _run((2, 1, 1), 8, 1, mode)
+
+
+@pytest.mark.parametrize("mode", ["directrace", "bulkrace"])
+def test_epochs_hold_under_jitter(mode):
+    """Each rank queues 0-3 seeded busy kernels before every exchange, so the four ranks' streams
+    drift apart; the race loop (rewrite, exchange, check, all on the stream) stays bit-exact over
+    400 exchanges. tools/epoch_soak.py runs the same at 10x the length on more layouts."""
+    _run((2, 2, 1), 12, 3, mode, reps=50, jitter=True)
+
+
+def test_race_check_sees_a_missing_epoch():
+    """Negative control of the race checks: the direct race loop with the epoch launch left out
+    must report cells of other exchanges (profiles/r04_epoch_soak.json: 41M bad cells at 500)."""
+    _run((2, 2, 1), 12, 3, "directnoepoch", reps=50, jitter=True, expect_bad=True)
