@@ -21,7 +21,9 @@ open / put-when-writable / wait sequence, bulk_communication_object.hpp:621-694)
                     them); wait until each of its targets has opened its halos
   puts           -> one k_put launch per group of <= 64 messages
   k_epoch(close) -> signal each target that this epoch's puts are in; wait until each source's are
-over a flag block in node-shared host memory (libghx ghx_epochs_*). Nothing blocks the host;
+with flags in each receiver's fine-grained device memory (its "inbox", IPC-mapped into its
+node-local peers and polled locally; a node-shared host block carries the inbox handles and each
+rank's epoch and error for the host: libghx ghx_epochs_*). Nothing blocks the host;
 only the ranks a rank exchanges with synchronise with it; wait() reports a peer that never
 arrived (bounded waits, `timeout` seconds). epochs="host" keeps the round-2 form: drain the
 stream, barrier, puts, drain, barrier. Puts go to node-local peers (ranks whose hostnames

@@ -443,9 +443,11 @@ int ghx_put_destroy(ghx_put* put);
  * access guards (include/ghex/rma/access_guard.hpp:35-140; per range: start/end_target_epoch on
  * the owner, start/end_source_epoch on the putter; include/ghex/bulk_communication_object.hpp
  * :621-694) as TWO stream-ordered launches around the data launch(es) — phase 0 (open) before,
- * phase 1 (close) after — over a flag block in node-shared host memory (POSIX shm `name`,
- * "/..."; the creating rank passes create = 1 before the others attach with 0, and one rank
- * unlinks the name once all have attached). `world` and `rank` are the node-local group's size
+ * phase 1 (close) after. The flags live in each rank's inbox, fine-grained device memory on its
+ * GPU that its node-local peers map through IPC and write into, polled locally; a block of
+ * node-shared host memory (POSIX shm `name`, "/...") carries the inbox handles and each rank's
+ * epoch and error for the host (the creating rank passes create = 1 before the others attach
+ * with 0, and one rank unlinks the name once all have attached). `world` and `rank` are the node-local group's size
  * and this rank's index in it (one block per host; at most 64 ranks per host). ghx_epochs_peers
  * sets this rank's sources (ranks that write into its memory) and targets (ranks whose memory it
  * writes into) as node-local indices, excluding itself. Open: this rank's halos / receive
