@@ -9,6 +9,8 @@ after the exchange — halos, interior and padding — equals the oracle's excha
 packed send buffer equals the oracle's bytes (alignment pads masked: the reference never writes
 them either, communication_object.hpp:1059-1065). The oracle follows
 include/ghex/structured/pattern.hpp:214-571 (patterns) and pack_kernels.hpp:62-158 (bytes)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -80,10 +82,12 @@ def _alloc(dom, f, halos_max, rng):
     return a, orc.FieldSpec(a, dt.itemsize, f["layout"], tuple(offs), tuple(exts))
 
 
-def run_case(case):
-    from ghex_amd import _ghx
+def _setup_case(case):
+    """Device fields, communication objects and buffer infos of every emulated rank, and the
+    oracle's exchange of the same fields (its packed buffers; its field arrays are updated in
+    place to the post-exchange state)."""
     from ghex_amd.structured import regular as R
-    from tests.gpu_util import FakeContext, device_field, emulated_exchange
+    from tests.gpu_util import FakeContext, device_field
     ranks, nr = case["ranks"], len(case["ranks"])
     gf, gl = (0, 0, 0), tuple(g - 1 for g in case["G"])
     per = case["periodic"]
@@ -111,32 +115,138 @@ def run_case(case):
         bis_all.append(bis)
         ranks_fields.append(rf)
     obufs = orc.regular_exchange(ranks_fields, pat_o, nr)
+    return dict(nr=nr, pat_o=pat_o, cos=cos, bis_all=bis_all, pairs=pairs,
+                ranks_fields=ranks_fields, obufs=obufs)
+
+
+def _check_buffer(st, r, x, got):
+    """A packed message (uint8 device tensor) against the oracle's bytes, pads masked."""
+    ob = st["obufs"][(r, x["pair"])]
+    assert ob.size == x["size"]
+    rf = st["ranks_fields"][r]
+    items = [(k, f[1], st["pat_o"][f[3]][r][f[2]], f[0].elem, f[0].data.dtype.alignment, 1, 0)
+             for k, f in enumerate(rf)]
+    b = orc.plan_buffers(items, receive=False)[x["pair"]]
+    m = np.zeros(b.size, dtype=bool)
+    for pf in b.fields:
+        elem = rf[pf.field_index][0].elem
+        n = sum(isp.size() for isp in pf.boxes) * elem
+        m[pf.offset:pf.offset + n] = True
+    np.testing.assert_array_equal(got[:x["size"]].cpu().numpy()[m], ob[m])
+
+
+def run_case(case):
+    from ghex_amd import _ghx
+    from tests.gpu_util import emulated_exchange
+    st = _setup_case(case)
     _ghx.call("ghx_tune", b"mixed_always", 1 if case["mixed"] else 0)
     try:
-        plans, bufs = emulated_exchange(cos, bis_all, mixed=case["mixed"])
+        plans, bufs = emulated_exchange(st["cos"], st["bis_all"], mixed=case["mixed"])
     finally:
         _ghx.call("ghx_tune", b"reset", 0)
-    for base, a in pairs:
+    for base, a in st["pairs"]:
         np.testing.assert_array_equal(base.cpu().numpy(), a)
-    for r in range(nr):
-        items = [(k, f[1], pat_o[f[3]][r][f[2]], f[0].elem, f[0].data.dtype.alignment, 1, 0)
-                 for k, f in enumerate(ranks_fields[r])]
-        pb = orc.plan_buffers(items, receive=False)
+    for r in range(st["nr"]):
         for i, x in enumerate(plans[r].send):
-            ob = obufs[(r, x["pair"])]
-            assert ob.size == x["size"]
-            b = pb[x["pair"]]
-            m = np.zeros(b.size, dtype=bool)
-            for pf in b.fields:
-                elem = ranks_fields[r][pf.field_index][0].elem
-                n = sum(isp.size() for isp in pf.boxes) * elem
-                m[pf.offset:pf.offset + n] = True
-            np.testing.assert_array_equal(bufs[r][0][i][:x["size"]].cpu().numpy()[m], ob[m])
+            _check_buffer(st, r, x, bufs[r][0][i])
+
+
+def _dbl(n):
+    return max(256, (n + 255) // 256 * 256)
+
+
+def run_case_direct(case):
+    """The same random case as the direct exchange runs it between processes: every peer
+    message packed straight into its receiver's buffer, which exists twice; the copy is chosen
+    on the device from an epoch word (ghx_exchange_set_parity: pack with the word at e - 1 and
+    add 1, unpack with it at e and add 0, as around the one-launch close). Exchange e = 1 and
+    e = 2 (both copies): every cell equals the oracle's exchange, every packed message equals
+    the oracle's bytes in copy e&1, and the other copy is untouched until its own exchange."""
+    import torch
+    from ghex_amd import _ghx
+    st = _setup_case(case)
+    cos, bis_all, nr = st["cos"], st["bis_all"], st["nr"]
+    L = _ghx.lib()
+    word = torch.zeros(1, dtype=torch.int64, device="cuda")
+    wp = ctypes.c_void_p(word.data_ptr())
+    plans = [co.plan(bis) for co, bis in zip(cos, bis_all)]
+    mixed = [case["mixed"] and co.mixed(p) for co, p in zip(cos, plans)]
+    # receive side: peer buffers twice (sentinel 0xA5), self messages alias their send buffer
+    own_send = [[torch.full((max(1, b["size"]),), 0x5A, dtype=torch.uint8, device="cuda")
+                 for b in p.send] for p in plans]
+    recv = []
+    for r, p in enumerate(plans):
+        rr = []
+        for b in p.recv:
+            j = next((i for i, sb in enumerate(p.send) if sb["pair"] == b["pair"] and b["rank"] == r),
+                     None)
+            rr.append(own_send[r][j] if j is not None else
+                      torch.full((2 * _dbl(b["size"]),), 0xA5, dtype=torch.uint8, device="cuda"))
+        recv.append(rr)
+    sptr, soff = [], []
+    for r, p in enumerate(plans):
+        ptrs, offs = [], []
+        for i, b in enumerate(p.send):
+            if b["rank"] == r:
+                ptrs.append(own_send[r][i].data_ptr())
+                offs.append(0)
+                continue
+            q = b["rank"]
+            k = next(k for k, rb in enumerate(plans[q].recv) if rb["pair"] == b["pair"] and rb["rank"] == r)
+            assert plans[q].recv[k]["size"] == b["size"] and plans[q].recv[k]["tag"] == b["tag"]
+            ptrs.append(recv[q][k].data_ptr())
+            offs.append(_dbl(b["size"]))
+        sptr.append(_ghx.ptr_array(ptrs))
+        soff.append(offs)
+        roff = [_dbl(b["size"]) if b["rank"] != r else 0 for b in p.recv]
+        for direction, add, o in ((0, 1, offs), (1, 0, roff)):
+            _ghx.call("ghx_exchange_set_parity", p.h, direction, wp, add,
+                      (ctypes.c_int64 * max(1, len(o)))(*o), len(o))
+    rptr = [_ghx.ptr_array([t.data_ptr() for t in rr]) for rr in recv]
+    fptr = [_ghx.ptr_array([bi.field.data_ptr() for bi in bis]) for bis in bis_all]
+    before = [base.clone() for base, _ in st["pairs"]]
+    s = torch.cuda.current_stream().cuda_stream
+    _ghx.call("ghx_tune", b"mixed_always", 1 if case["mixed"] else 0)
+    try:
+        for e in (1, 2):
+            for (base, _), b0 in zip(st["pairs"], before):
+                base.copy_(b0)
+            word.fill_(e - 1)
+            for r, p in enumerate(plans):
+                fn = L.ghx_exchange_pack_self if mixed[r] else L.ghx_exchange_pack
+                _ghx.check(fn(p.h, fptr[r], len(bis_all[r]), sptr[r], len(p.send), s), "pack")
+            word.fill_(e)
+            for r, p in enumerate(plans):
+                fn = L.ghx_exchange_unpack_peers if mixed[r] else L.ghx_exchange_unpack
+                _ghx.check(fn(p.h, fptr[r], len(bis_all[r]), rptr[r], len(p.recv), s), "unpack")
+            torch.cuda.synchronize()
+            for base, a in st["pairs"]:
+                np.testing.assert_array_equal(base.cpu().numpy(), a)
+            for r, p in enumerate(plans):
+                for i, b in enumerate(p.recv):
+                    if b["rank"] == r:
+                        continue
+                    q = b["rank"]
+                    x = next(x for x in plans[q].send if x["pair"] == b["pair"] and x["rank"] == r)
+                    d = _dbl(b["size"])
+                    live = recv[r][i][d * (e & 1):]
+                    _check_buffer(st, q, x, live)
+                    if e == 1:  # copy 0 not yet written
+                        assert bool((recv[r][i][:b["size"]] == 0xA5).all())
+    finally:
+        _ghx.call("ghx_tune", b"reset", 0)
 
 
 @pytest.mark.parametrize("seed", range(60))
 def test_random_structured_exchange(seed):
     run_case(draw_case(seed))
+
+
+@pytest.mark.parametrize("seed", range(200, 230))
+def test_random_direct_double_buffered_exchange(seed):
+    """The seeded random cases through the direct exchange's launches: packs into the receivers'
+    double-buffered buffers, copies chosen on the device (run_case_direct)."""
+    run_case_direct(draw_case(seed))
 
 
 def test_more_slots_than_one_launch_holds():

@@ -4,7 +4,9 @@ ranges far beyond the suite's 60 structured / 40 unstructured seeds, within a ti
 seed is the suite's own case (draw_case / draw_unstructured) checked the suite's own way (every
 cell against the oracle's exchange, every packed byte against the oracle's buffer). One progress
 line per 25 seeds on stderr; one JSON summary line on stdout with every failing seed and its
-error. usage: python tools/fuzz_soak.py --structured 60:2000 --unstructured 40:2000 --seconds 400"""
+error. --direct runs the same structured cases through the direct exchange's double-buffered
+launches (run_case_direct). usage: python tools/fuzz_soak.py --structured 60:2000
+--unstructured 40:2000 --direct 230:2000 --seconds 400"""
 import argparse
 import json
 import os
@@ -20,6 +22,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--structured", default="60:1000")
     p.add_argument("--unstructured", default="40:1000")
+    p.add_argument("--direct", default="0:0",
+                   help="seed range of the double-buffered direct form (run_case_direct)")
     p.add_argument("--seconds", type=float, default=300)
     a = p.parse_args()
     import torch
@@ -29,9 +33,12 @@ def main():
     ghex_amd.native_library()
     from tests import test_gpu_fuzz as F
     t0 = time.time()
-    out = {"structured": {"ran": 0, "failed": []}, "unstructured": {"ran": 0, "failed": []}}
+    out = {"structured": {"ran": 0, "failed": []}, "unstructured": {"ran": 0, "failed": []},
+           "direct": {"ran": 0, "failed": []}}
     kinds = [("structured", a.structured, lambda s: F.run_case(F.draw_case(s))),
-             ("unstructured", a.unstructured, lambda s: F.run_unstructured(F.draw_unstructured(s)))]
+             ("unstructured", a.unstructured, lambda s: F.run_unstructured(F.draw_unstructured(s))),
+             ("direct", a.direct, lambda s: F.run_case_direct(F.draw_case(s)))]
+    kinds = [k for k in kinds if k[1].split(":")[0] != k[1].split(":")[1]]
     share = a.seconds / len(kinds)
     for i, (name, rng, fn) in enumerate(kinds):
         lo, hi = (int(x) for x in rng.split(":"))
@@ -53,7 +60,7 @@ def main():
                       f"{time.time() - t0:.0f} s", file=sys.stderr, flush=True)
     out["seconds"] = round(time.time() - t0, 1)
     print(json.dumps(out), flush=True)
-    return 1 if out["structured"]["failed"] or out["unstructured"]["failed"] else 0
+    return 1 if any(v["failed"] for v in out.values() if isinstance(v, dict)) else 0
 
 
 if __name__ == "__main__":
