@@ -9,8 +9,6 @@ after the exchange — halos, interior and padding — equals the oracle's excha
 packed send buffer equals the oracle's bytes (alignment pads masked: the reference never writes
 them either, communication_object.hpp:1059-1065). The oracle follows
 include/ghex/structured/pattern.hpp:214-571 (patterns) and pack_kernels.hpp:62-158 (bytes)."""
-import ctypes
-
 import numpy as np
 import pytest
 
@@ -151,90 +149,33 @@ def run_case(case):
             _check_buffer(st, r, x, bufs[r][0][i])
 
 
-def _dbl(n):
-    return max(256, (n + 255) // 256 * 256)
-
-
 def run_case_direct(case):
-    """The same random case as the direct exchange runs it between processes: every peer
-    message packed straight into its receiver's buffer, which exists twice; the copy is chosen
-    on the device from an epoch word (ghx_exchange_set_parity: pack with the word at e - 1 and
-    add 1, unpack with it at e and add 0, as around the one-launch close). Exchange e = 1 and
-    e = 2 (both copies): every cell equals the oracle's exchange, every packed message equals
-    the oracle's bytes in copy e&1, and the other copy is untouched until its own exchange."""
-    import torch
+    """The same random case as the direct exchange runs it between processes
+    (tests.gpu_util.EmulatedDirect: packs into the receivers' double-buffered buffers, the copy
+    chosen on the device). Exchange e = 1 and e = 2 (both copies), each from the pre-exchange
+    fields: every cell equals the oracle's exchange, every packed message equals the oracle's
+    bytes in copy e&1, and copy 0 is untouched by exchange 1. Returns the peer messages checked."""
     from ghex_amd import _ghx
+    from tests.gpu_util import EmulatedDirect
     st = _setup_case(case)
-    cos, bis_all, nr = st["cos"], st["bis_all"], st["nr"]
-    L = _ghx.lib()
-    word = torch.zeros(1, dtype=torch.int64, device="cuda")
-    wp = ctypes.c_void_p(word.data_ptr())
-    plans = [co.plan(bis) for co, bis in zip(cos, bis_all)]
-    mixed = [case["mixed"] and co.mixed(p) for co, p in zip(cos, plans)]
-    # receive side: peer buffers twice (sentinel 0xA5), self messages alias their send buffer
-    own_send = [[torch.full((max(1, b["size"]),), 0x5A, dtype=torch.uint8, device="cuda")
-                 for b in p.send] for p in plans]
-    recv = []
-    for r, p in enumerate(plans):
-        rr = []
-        for b in p.recv:
-            j = next((i for i, sb in enumerate(p.send) if sb["pair"] == b["pair"] and b["rank"] == r),
-                     None)
-            rr.append(own_send[r][j] if j is not None else
-                      torch.full((2 * _dbl(b["size"]),), 0xA5, dtype=torch.uint8, device="cuda"))
-        recv.append(rr)
-    sptr, soff = [], []
-    for r, p in enumerate(plans):
-        ptrs, offs = [], []
-        for i, b in enumerate(p.send):
-            if b["rank"] == r:
-                ptrs.append(own_send[r][i].data_ptr())
-                offs.append(0)
-                continue
-            q = b["rank"]
-            k = next(k for k, rb in enumerate(plans[q].recv) if rb["pair"] == b["pair"] and rb["rank"] == r)
-            assert plans[q].recv[k]["size"] == b["size"] and plans[q].recv[k]["tag"] == b["tag"]
-            ptrs.append(recv[q][k].data_ptr())
-            offs.append(_dbl(b["size"]))
-        sptr.append(_ghx.ptr_array(ptrs))
-        soff.append(offs)
-        roff = [_dbl(b["size"]) if b["rank"] != r else 0 for b in p.recv]
-        for direction, add, o in ((0, 1, offs), (1, 0, roff)):
-            _ghx.call("ghx_exchange_set_parity", p.h, direction, wp, add,
-                      (ctypes.c_int64 * max(1, len(o)))(*o), len(o))
-    rptr = [_ghx.ptr_array([t.data_ptr() for t in rr]) for rr in recv]
-    fptr = [_ghx.ptr_array([bi.field.data_ptr() for bi in bis]) for bis in bis_all]
     before = [base.clone() for base, _ in st["pairs"]]
-    s = torch.cuda.current_stream().cuda_stream
     _ghx.call("ghx_tune", b"mixed_always", 1 if case["mixed"] else 0)
     try:
+        dx = EmulatedDirect(st["cos"], st["bis_all"], mixed=case["mixed"])
+        msgs = dx.peer_messages()
         for e in (1, 2):
             for (base, _), b0 in zip(st["pairs"], before):
                 base.copy_(b0)
-            word.fill_(e - 1)
-            for r, p in enumerate(plans):
-                fn = L.ghx_exchange_pack_self if mixed[r] else L.ghx_exchange_pack
-                _ghx.check(fn(p.h, fptr[r], len(bis_all[r]), sptr[r], len(p.send), s), "pack")
-            word.fill_(e)
-            for r, p in enumerate(plans):
-                fn = L.ghx_exchange_unpack_peers if mixed[r] else L.ghx_exchange_unpack
-                _ghx.check(fn(p.h, fptr[r], len(bis_all[r]), rptr[r], len(p.recv), s), "unpack")
-            torch.cuda.synchronize()
+            dx.exchange(e)
             for base, a in st["pairs"]:
                 np.testing.assert_array_equal(base.cpu().numpy(), a)
-            for r, p in enumerate(plans):
-                for i, b in enumerate(p.recv):
-                    if b["rank"] == r:
-                        continue
-                    q = b["rank"]
-                    x = next(x for x in plans[q].send if x["pair"] == b["pair"] and x["rank"] == r)
-                    d = _dbl(b["size"])
-                    live = recv[r][i][d * (e & 1):]
-                    _check_buffer(st, q, x, live)
-                    if e == 1:  # copy 0 not yet written
-                        assert bool((recv[r][i][:b["size"]] == 0xA5).all())
+            for r, i, q, x, d in msgs:
+                _check_buffer(st, q, x, dx.recv[r][i][d * (e & 1):])
+                if e == 1:  # copy 0 not yet written
+                    assert bool((dx.recv[r][i][:x["size"]] == 0xA5).all())
     finally:
         _ghx.call("ghx_tune", b"reset", 0)
+    return len(msgs)
 
 
 @pytest.mark.parametrize("seed", range(60))
@@ -332,10 +273,10 @@ def _ufield(torch, n, f, rng):
     return t, view, a
 
 
-def run_unstructured(case):
+def _setup_unstructured(case):
     import torch
     from ghex_amd import unstructured as U
-    from tests.gpu_util import FakeContext, emulated_exchange
+    from tests.gpu_util import FakeContext
     nr = case["nr"]
     table = {r: [(d["id"], d["gids"], d["outer"], None) for d in case["doms"] if d["rank"] == r]
              for r in range(nr)}
@@ -354,9 +295,12 @@ def run_unstructured(case):
                 recs.append((f, d, t, a))
         cos.append(U.make_communication_object(ctx))
         bis_all.append(bis)
-    emulated_exchange(cos, bis_all)
-    # expected: every outer cell holds, on every level, the value of the cell that owns its gid
-    for fi, f in enumerate(case["fields"]):
+    return cos, bis_all, recs
+
+
+def _check_unstructured(case, recs):
+    """Every outer cell holds, on every level, the value of the cell that owns its gid."""
+    for f in case["fields"]:
         owner = {}
         for (ff, d, t, a) in recs:
             if ff is not f:
@@ -379,9 +323,44 @@ def run_unstructured(case):
             np.testing.assert_array_equal(got.view(np.uint8), exp.view(np.uint8))
 
 
+def run_unstructured(case):
+    from tests.gpu_util import emulated_exchange
+    cos, bis_all, recs = _setup_unstructured(case)
+    emulated_exchange(cos, bis_all)
+    _check_unstructured(case, recs)
+
+
+def run_unstructured_direct(case):
+    """A random unstructured case through the direct exchange's double-buffered launches
+    (tests.gpu_util.EmulatedDirect; index-list and run-path kernels alike): exchanges 1 and 2,
+    each from the pre-exchange fields, every field byte checked, copy 0 untouched by exchange 1.
+    Returns the peer messages checked."""
+    from tests.gpu_util import EmulatedDirect
+    cos, bis_all, recs = _setup_unstructured(case)
+    before = [t.clone() for (_, _, t, _) in recs]
+    dx = EmulatedDirect(cos, bis_all)
+    msgs = dx.peer_messages()
+    for e in (1, 2):
+        for (_, _, t, _), b0 in zip(recs, before):
+            t.copy_(b0)
+        dx.exchange(e)
+        _check_unstructured(case, recs)
+        if e == 1:
+            for r, i, q, x, d in msgs:
+                assert bool((dx.recv[r][i][:x["size"]] == 0xA5).all())
+    return len(msgs)
+
+
 @pytest.mark.parametrize("seed", range(40))
 def test_random_unstructured_exchange(seed):
     run_unstructured(draw_unstructured(seed))
+
+
+@pytest.mark.parametrize("seed", range(100, 120))
+def test_random_unstructured_direct_double_buffered_exchange(seed):
+    """The seeded random unstructured cases through the direct exchange's launches
+    (run_unstructured_direct)."""
+    run_unstructured_direct(draw_unstructured(seed))
 
 
 def test_unstructured_more_buffers_than_one_launch_holds():

@@ -24,6 +24,8 @@ def main():
     p.add_argument("--unstructured", default="40:1000")
     p.add_argument("--direct", default="0:0",
                    help="seed range of the double-buffered direct form (run_case_direct)")
+    p.add_argument("--udirect", default="0:0",
+                   help="seed range of the unstructured direct form (run_unstructured_direct)")
     p.add_argument("--seconds", type=float, default=300)
     a = p.parse_args()
     import torch
@@ -34,10 +36,11 @@ def main():
     from tests import test_gpu_fuzz as F
     t0 = time.time()
     out = {"structured": {"ran": 0, "failed": []}, "unstructured": {"ran": 0, "failed": []},
-           "direct": {"ran": 0, "failed": []}}
+           "direct": {"ran": 0, "failed": []}, "udirect": {"ran": 0, "failed": []}}
     kinds = [("structured", a.structured, lambda s: F.run_case(F.draw_case(s))),
              ("unstructured", a.unstructured, lambda s: F.run_unstructured(F.draw_unstructured(s))),
-             ("direct", a.direct, lambda s: F.run_case_direct(F.draw_case(s)))]
+             ("direct", a.direct, lambda s: F.run_case_direct(F.draw_case(s))),
+             ("udirect", a.udirect, lambda s: F.run_unstructured_direct(F.draw_unstructured(s)))]
     kinds = [k for k in kinds if k[1].split(":")[0] != k[1].split(":")[1]]
     share = a.seconds / len(kinds)
     for i, (name, rng, fn) in enumerate(kinds):
@@ -49,7 +52,9 @@ def main():
             if time.time() > stop:
                 break
             try:
-                fn(seed)
+                got = fn(seed)
+                if isinstance(got, int):  # the direct forms: peer messages checked
+                    rec["peer_messages"] = rec.get("peer_messages", 0) + got
             except Exception as e:
                 rec["failed"].append({"seed": seed, "error": f"{type(e).__name__}: {str(e)[:300]}",
                                       "where": traceback.format_exc()[-600:]})
