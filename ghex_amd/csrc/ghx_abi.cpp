@@ -1242,6 +1242,8 @@ int ghx_exchange_set_parity(ghx_exchange* ex, int32_t direction, const uint64_t*
             if (ex->uunpack) ex->uunpack->parity = cfg;
             if (ex->punpack) ex->punpack->parity = cfg;
         }
+        ex->dir_parity[direction] = cfg;
+        if (ex->split) ex->set_split_parity(direction);
         return GHX_OK;
     });
 }

@@ -32,6 +32,7 @@ struct exchange_plan
     std::unique_ptr<splan> punpack;
     bool mixed = false;
     parity_cfg mixed_parity;  // the mixed pack launch's double-buffered send buffers (direct)
+    parity_cfg dir_parity[2];  // ghx_exchange_set_parity per direction (the per-buffer plans too)
     int32_t n_items = 0;
     mutable int self_ok = -1;  // lazily checked: may pack and unpack be fused (all self)?
 
@@ -71,6 +72,16 @@ struct exchange_plan
             }
         }
         split = true;
+        for (int dir = 0; dir < 2; ++dir) set_split_parity(dir);
+    }
+
+    // the per-buffer plans use the copies ghx_exchange_set_parity selected, like the whole ones
+    void set_split_parity(int dir)
+    {
+        for (auto& p : bplan[dir])
+            if (p) p->parity = dir_parity[dir];
+        for (auto& p : ubplan[dir])
+            if (p) p->parity = dir_parity[dir];
     }
 
     // one buffer's pack (dir 0) or unpack (dir 1); the pointer arrays are the whole exchange's

@@ -398,8 +398,9 @@ int ghx_exchange_unpack_peers(const ghx_exchange* ex, void* const* field_ptrs, i
                               void* const* recv_buffers, int32_t n_recv, ghx_stream stream);
 
 /* Double-buffered buffers (the direct exchange's one-launch epochs, ghx_epochs_enqueue phase 2):
- * every later pack (direction 0: ghx_exchange_pack, _pack_self) or unpack (1: ghx_exchange_unpack,
- * _unpack_peers) launch of `ex` uses, for buffer i with offsets[i] != 0, the copy at
+ * every later pack (direction 0: ghx_exchange_pack, _pack_self, _pack_buffer) or unpack (1:
+ * ghx_exchange_unpack, _unpack_peers, _unpack_buffer) launch of `ex` uses, for buffer i with
+ * offsets[i] != 0, the copy at
  * buffer_ptr + offsets[i] when (*parity_word + parity_add) is odd, read on the device at launch
  * (a captured graph alternates on replay). offsets: one per buffer of that direction, multiples
  * of 256 B (0 = one copy). parity_word = NULL restores single buffers. The reference has no

@@ -61,18 +61,23 @@ def _set(plan, direction, word, add, offsets):
               (ctypes.c_int64 * max(1, len(offsets)))(*offsets), len(offsets))
 
 
-@pytest.mark.parametrize("parts,N,Hw,nf", [((2, 1, 1), 12, 2, 1), ((2, 2, 1), 9, 1, 1),
-                                           ((1, 1, 2), 10, 3, 1), ((2, 1, 1), 6, 1, 70)])
-@pytest.mark.parametrize("mixed", [False, True])
-@pytest.mark.parametrize("graph", [False, True])
-def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, nf, mixed, graph):
+_GEOMS = [((2, 1, 1), 12, 2, 1), ((2, 2, 1), 9, 1, 1), ((1, 1, 2), 10, 3, 1), ((2, 1, 1), 6, 1, 70)]
+
+
+@pytest.mark.parametrize("parts,N,Hw,nf,mixed,graph,form",
+                         [g + (m, gr, "whole") for g in _GEOMS for m in (False, True)
+                          for gr in (False, True)] +
+                         [g + (False, False, "per_buffer") for g in _GEOMS])
+def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, nf, mixed, graph, form):
     """Each rank's send buffers and peer receive buffers exist twice (the odd copy at
     _dbl(size)). Exchange k packs with the device word at k - 1 and add 1, as before the epoch
     close, then unpacks with the word at k and add 0, as after it: both select copy k&1, and the
     test routes the packed copy into the receiver's copy of the same parity in between. Every
     packed byte must land in the selected copy only, and every cell must come out right — with
     the launches eager, or captured once and replayed; 70 fields cut the plans into launch
-    groups (each with its own slot map of the copies' offsets)."""
+    groups (each with its own slot map of the copies' offsets). form="per_buffer": the same
+    through the per-buffer launches (ghx_exchange_split + ghx_exchange_pack_buffer /
+    unpack_buffer, one launch per buffer), which must select the same copies."""
     import torch
     from ghex_amd import _ghx
     rs = _ranks(parts, N, Hw, nf)
@@ -102,13 +107,27 @@ def test_launches_use_the_copy_of_the_device_parity(parts, N, Hw, nf, mixed, gra
                        sp=_ghx.ptr_array([t.data_ptr() for t in send]),
                        rp=_ghx.ptr_array([t.data_ptr() for t in recv])))
 
+    if form == "per_buffer":
+        for x in st:
+            _ghx.call("ghx_exchange_split", x["plan"].h)
+
     def pack(s):
         for x in st:
+            if form == "per_buffer":
+                for i in range(len(x["send"])):
+                    _ghx.check(L.ghx_exchange_pack_buffer(x["plan"].h, i, x["f"], len(x["bis"]),
+                                                          x["sp"], len(x["send"]), s), "pack_buffer")
+                continue
             fn = L.ghx_exchange_pack_self if x["mixed"] else L.ghx_exchange_pack
             _ghx.check(fn(x["plan"].h, x["f"], len(x["bis"]), x["sp"], len(x["send"]), s), "pack")
 
     def unpack(s):
         for x in st:
+            if form == "per_buffer":
+                for i in range(len(x["recv"])):
+                    _ghx.check(L.ghx_exchange_unpack_buffer(x["plan"].h, i, x["f"], len(x["bis"]),
+                                                            x["rp"], len(x["recv"]), s), "unpack_buffer")
+                continue
             fn = L.ghx_exchange_unpack_peers if x["mixed"] else L.ghx_exchange_unpack
             _ghx.check(fn(x["plan"].h, x["f"], len(x["bis"]), x["rp"], len(x["recv"]), s), "unpack")
 
