@@ -55,6 +55,8 @@ def parse():
                    help="steps captured per hipGraph (the K timed steps replay K/G graphs); "
                         "0: all K steps in one graph (at most 1000)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-config-seconds", type=float, default=3.0,
+                   help="seconds of CPU work for each extra config's cpu_baseline (configs 4, 5)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     p.add_argument("--tune", default="", help="developer: ghx_tune key=value,... before planning")
@@ -891,8 +893,8 @@ def extras(args, torch, dist, dev, stream, out, v):
             out["exchange_pipelined"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
         co.exchange(bis).wait()  # halos valid again
     if world > 1:
-        # the unstructured path between real ranks (BASELINE config 5's shape, scaled to 1M cells
-        # per rank so the setup all-gather stays small): verified and timed
+        # the unstructured path between real ranks at BASELINE config 5's size (10M cells per
+        # rank; the pattern built from reduced halos): setup time, verified, timed
         try:
             out["unstructured_exchange"] = bench_unstructured(v, torch, dist, dev, args)
         except Exception as e:  # reported; the legs after it still run
@@ -1001,11 +1003,19 @@ def extras(args, torch, dist, dev, stream, out, v):
         del bis, send, recv
         co = None
         torch.cuda.empty_cache()
-        out["extra_configs"] = {
-            "config4_5fields_256^3_h3_f64f32": bench_config4(torch, dev, ghex_amd, R),
-            "config5_unstructured_10M_5pct_levels1": bench_config5(torch, dev, _ghx, 1),
-            "config5_unstructured_10M_5pct_levels8": bench_config5(torch, dev, _ghx, 8),
-        }
+        cs = None if (rank != 0 or args.no_cpu_baseline) else args.cpu_config_seconds
+        ex = out["extra_configs"] = {}
+        ex["config4_5fields_256^3_h3_f64f32"] = bench_config4(torch, dev, ghex_amd, R, cs)
+        pats, t_all, t_rank = config5_patterns()
+        for lv in (1, 8):
+            ex[f"config5_unstructured_10M_5pct_levels{lv}"] = bench_config5(
+                torch, dev, _ghx, lv, pats, cs)
+        ex["config5_pattern_setup"] = {
+            "ranks": 8, "cells_per_rank": int(pats[0][0].size - pats[0][1].size),
+            "seconds_all_ranks": round(t_all, 2), "seconds_max_rank": round(t_rank, 2),
+            "what": "8 ranks as threads of this process (LoopbackWorld), each generating its "
+                    "domain and running the product make_pattern<unstructured> (reduced halos)"}
+        del pats
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, Hw, args.cpu_seconds)
 
@@ -1252,52 +1262,61 @@ def kernel_durations(torch, dev, stream, fns, M=10, rounds=31):
     return tuple(out)
 
 
-def bench_unstructured(v, torch, dist, dev, args, cells=1_000_000, frac=20):
-    """BASELINE config 5 between the real ranks, scaled: every rank owns `cells` cells (gids
-    rank*10^7 + i) and holds cells/frac halo cells drawn from the other ranks' (seed 20260715 +
-    rank), in a randomly permuted local storage order; value = gid*100 (levels 1, fp64). One
-    CommunicationObject.exchange per step over the context's transport (RCCL; gloo + host staging
-    in a rehearsal); every halo value checked; bytes per rank and step 4 * halo * 8."""
+def bench_unstructured(v, torch, dist, dev, args, cells=None):
+    """BASELINE config 5 between the real ranks at its size: every rank's domain from
+    tools/config5_gen.cpp (10M cells, gids rank*10^7 + i, 5 % halo from the other ranks,
+    mt19937_64 seed 20260715, permuted storage), the product make_pattern<unstructured> over the
+    context (reduced halos, timed as setup_s, max over ranks), levels 1, fp64, value gid*100.
+    One CommunicationObject.exchange per step over the context's transport (RCCL; gloo + host
+    staging in a rehearsal); `verified`: after the timed region, outer cells reset to -1, one
+    more exchange, every cell of every rank checked. Bytes per rank and step: 2 * (sent +
+    received values) * 8."""
     import numpy as np
     from ghex_amd import unstructured as U
+    from tools import config5 as C5
     rank, world, ctx, K = v["rank"], v["world"], v["ctx"], v["K"]
-    rng = np.random.default_rng(20260715 + rank)
-    nh = cells // frac
-    others = np.array([r for r in range(world) if r != rank])
-    owner = others[rng.integers(0, len(others), size=4 * nh)]
-    local = rng.integers(0, cells, size=4 * nh)
-    halo = np.unique(owner.astype(np.int64) * 10_000_000 + local)
-    halo = rng.permutation(halo)[:nh]
-    gids = np.concatenate([rank * 10_000_000 + np.arange(cells, dtype=np.int64), halo])
-    perm = rng.permutation(len(gids))
-    gids = gids[perm]
-    outer = np.nonzero(perm >= cells)[0]  # storage positions of the halo cells
-    dd = U.DomainDescriptor(rank, gids.tolist(), outer.tolist())
+    cells = C5.CELLS if cells is None else cells
+    gids, outer = C5.generate(rank, world, cells)
+    red = v["all_reduce_host"]
+    red(0.0, dist.ReduceOp.SUM)  # start the setup clock together
+    t0 = time.perf_counter()
+    dd = U.DomainDescriptor(rank, gids, outer)
     pc = U.make_pattern(ctx, U.HaloGenerator(), [dd])
-    init = gids.astype(np.float64) * 100.0
-    init[outer] = -1.0
-    field = torch.from_numpy(init).to(dev)
+    t_setup = red(time.perf_counter() - t0, dist.ReduceOp.MAX)
+    n_send = sum(len(l) for *_, l in pc.lid_arrays(0, 0))
+    want = torch.from_numpy(gids.astype(np.float64) * 100.0).to(dev)
+    field = want.clone()
+    out_t = torch.from_numpy(outer).to(dev)
+    field[out_t] = -1.0
     fd = U.make_field_descriptor(dd, field)
     co = U.make_communication_object(ctx, staging="host" if args.rehearse else None)
     bis = [pc(fd)]
+
+    def count_bad():
+        torch.cuda.synchronize(dev)
+        return int(red(float((field != want).sum().item()), dist.ReduceOp.SUM))
     co.exchange(bis).wait()
-    got = field.cpu().numpy()
-    bad = int((got[outer] != gids[outer].astype(np.float64) * 100.0).sum())
-    if world > 1:
-        t = torch.tensor([float(bad)], dtype=torch.float64, device="cpu" if args.rehearse else dev)
-        dist.all_reduce(t)
-        bad = int(t.item())
+    bad_first = count_bad()
     ke = min(K, 50)
     for _ in range(3):
         co.exchange(bis).wait()
     T = v["timed"](lambda: co.exchange(bis).wait(), ke)
-    nbytes = 4 * nh * 8
-    out = {"cells_per_rank": cells, "halo_cells_per_rank": nh, "peers": int(len(others)),
+    field[out_t] = -1.0
+    co.exchange(bis).wait()
+    bad = count_bad()
+    nbytes = 2 * (n_send + outer.size) * 8
+    out = {"cells_per_rank": cells, "halo_cells_per_rank": int(outer.size),
+           "send_cells_rank0": n_send, "peers": len(pc.lid_arrays(0, 0)),
+           "setup_s": round(t_setup, 3),
+           "setup_what": "DomainDescriptor + make_pattern<unstructured> (reduced halos), max "
+                         "over ranks",
            "ms_per_exchange": round(T / ke * 1e3, 4),
            "GBps_per_rank_algorithmic": round(nbytes * ke / T / 1e9, 2),
            "transport": "gloo + host staging (rehearsal)" if args.rehearse else "RCCL",
-           "verified": bad == 0}
-    del co, bis, fd, field
+           "verified": bad == 0 and bad_first == 0,
+           "verified_what": "first exchange, and one exchange after the timed region on outer "
+                            "cells reset to -1: every cell of every rank"}
+    del co, bis, fd, field, want
     torch.cuda.empty_cache()
     return out
 
@@ -1461,7 +1480,8 @@ def cold_duration(torch, dev, stream, fn, flush, M=10, rounds=7):
     return (med[1] - med[0]) / M
 
 
-def _time_graph(torch, dev, fn, k=50, per=10):
+def _graph_of(torch, dev, fn, per=10):
+    """A hipGraph of `per` back-to-back calls of fn (one eager call first, on a side stream)."""
     stream = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(dev)
     side.wait_stream(stream)
@@ -1472,38 +1492,63 @@ def _time_graph(torch, dev, fn, k=50, per=10):
     with torch.cuda.graph(g):
         for _ in range(per):
             fn(torch.cuda.current_stream(dev).cuda_stream)
+    return g
+
+
+def _time_graph(torch, dev, fn, k=50, per=10, keep=None):
+    """Seconds per call of fn, from replays of a graph of `per` calls (k calls in all); with
+    keep = a dict, the graph is returned in keep["graph"] (to replay the timed launches again
+    for verification)."""
+    g = _graph_of(torch, dev, fn, per)
     g.replay()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(k // per):
         g.replay()
     torch.cuda.synchronize(dev)
+    if keep is not None:
+        keep["graph"] = g
     return (time.perf_counter() - t0) / (k // per * per)
 
 
-def bench_config4(torch, dev, ghex_amd, R):
+CONFIG4_TYPES = ("f64", "f32", "f64", "f32", "f64")
+
+
+def bench_config4(torch, dev, ghex_amd, R, cpu_seconds=None):
     """BASELINE config 4 on one GPU: 5 fields 256^3 [f64,f32,f64,f32,f64], H=3, one exchange of
-    all five (one periodic domain: all self messages -> the fused launch), verified."""
+    all five (one periodic domain: all self messages). Timed: the per-rank form every rank runs
+    at N>1, one fused pack launch + one fused unpack launch over all five fields (hipGraph of
+    10); `verified`: that timed graph replayed once on halos reset to -1 and buffers set to 0xFF,
+    every cell of every field checked. `verified_fused`: the first co.exchange() (the fused
+    k_self launch). cpu_baseline: the oracle's single-thread serializer on the same five fields
+    (cpu_seconds None: skipped)."""
     from ghex_amd import _ghx
     N, H = 256, 3
     E = N + 2 * H
-    types = [torch.float64, torch.float32, torch.float64, torch.float32, torch.float64]
+    types = [torch.float64 if t == "f64" else torch.float32 for t in CONFIG4_TYPES]
     ctx = ghex_amd.make_context()
     dd = R.DomainDescriptor(0, (0, 0, 0), (N - 1,) * 3)
     pc = R.make_pattern(ctx, R.HaloGenerator((0, 0, 0), (N - 1,) * 3, (H,) * 6, (True,) * 3), [dd])
-    fields, bis = [], []
+    fields, bis, interiors = [], [], []
     ar = torch.arange(N, device=dev, dtype=torch.float64)
     val = (ar.view(1, 1, N) + N * (ar.view(1, N, 1) + N * ar.view(N, 1, 1)))
     for k, T in enumerate(types):
         f = torch.full((E, E, E), -1, dtype=T, device=dev)
         f[H:H + N, H:H + N, H:H + N] = ((val + k) % (1 << 23)).to(T)
         fields.append(f)
+        interiors.append(f[H:H + N, H:H + N, H:H + N].clone())
         bis.append(pc(R.make_field_descriptor(dd, f.permute(2, 1, 0), (H,) * 3, (E,) * 3)))
-    co = R.make_communication_object(ctx)
-    co.exchange(bis).wait()
+    del val
     idx = (torch.arange(E, device=dev) - H) % N
     wv = (idx.view(1, 1, E) + N * (idx.view(1, E, 1) + N * idx.view(E, 1, 1))).to(torch.float64)
-    ok = all(bool((f == ((wv + k) % (1 << 23)).to(f.dtype)).all()) for k, f in enumerate(fields))
+
+    def all_ok():
+        return all(bool((f == ((wv + k) % (1 << 23)).to(f.dtype)).all())
+                   for k, f in enumerate(fields))
+
+    co = R.make_communication_object(ctx)
+    co.exchange(bis).wait()
+    ok_fused = all_ok()
     plan = co.plan(bis)
     send, recv = co.buffers(plan, dev)
     fptr = _ghx.ptr_array([f.data_ptr() for f in fields])
@@ -1511,44 +1556,103 @@ def bench_config4(torch, dev, ghex_amd, R):
     L = _ghx.lib()
     fusedp = co.all_self(plan)
 
-    def step(s):
-        if fusedp:
-            L.ghx_exchange_self(plan.h, fptr, 5, sptr, len(send), s)
-        else:
-            two(s)
+    def fused(s):
+        _ghx.check(L.ghx_exchange_self(plan.h, fptr, 5, sptr, len(send), s), "exchange_self")
 
-    def two(s):  # the per-rank form at N>1: pack launch + unpack launch
-        L.ghx_exchange_pack(plan.h, fptr, 5, sptr, len(send), s)
-        L.ghx_exchange_unpack(plan.h, fptr, 5, sptr, len(send), s)
-    t = _time_graph(torch, dev, step)
-    t2 = _time_graph(torch, dev, two)
+    def two(s):  # the per-rank form at N>1: pack launch + unpack launch (self: recv IS send)
+        _ghx.check(L.ghx_exchange_pack(plan.h, fptr, 5, sptr, len(send), s), "pack")
+        _ghx.check(L.ghx_exchange_unpack(plan.h, fptr, 5, sptr, len(send), s), "unpack")
+    t = _time_graph(torch, dev, fused) if fusedp else None
+    keep = {}
+    t2 = _time_graph(torch, dev, two, keep=keep)
+    # verify the timed two-launch graph itself
+    for f, inner in zip(fields, interiors):
+        f.fill_(-1)
+        f[H:H + N, H:H + N, H:H + N] = inner
+    for b in send:
+        b.fill_(0xFF)
+    torch.cuda.synchronize(dev)
+    keep["graph"].replay()
+    torch.cuda.synchronize(dev)
+    ok = all_ok()
+    del keep
     n = E ** 3 - N ** 3
     nbytes = 4 * n * (3 * 8 + 2 * 4)
-    return {"GBps": round(nbytes / t2 / 1e9, 1), "frac": round(nbytes / t2 / 1e9 / HBM_PEAK_GBS, 4),
-            "us_per_exchange": round(t2 * 1e6, 2),
-            "bytes_per_exchange": nbytes, "verified": ok, "form": "pack launch + unpack launch",
-            "fused_self": {"us_per_exchange": round(t * 1e6, 2),
-                           "bytes_moved": 3 * n * (3 * 8 + 2 * 4)} if fusedp else None}
+    out = {"GBps": round(nbytes / t2 / 1e9, 1), "frac": round(nbytes / t2 / 1e9 / HBM_PEAK_GBS, 4),
+           "us_per_exchange": round(t2 * 1e6, 2),
+           "bytes_per_exchange": nbytes, "form": "pack launch + unpack launch",
+           "verified": ok,
+           "verified_what": "the timed hipGraph (10 x (pack + unpack) of all 5 fields) replayed "
+                            "once on halos reset to -1 and buffers set to 0xFF; every cell of "
+                            "every field checked",
+           "verified_fused": ok_fused,
+           "verified_fused_what": "the first co.exchange() (the fused k_self launch)",
+           "fused_self": {"us_per_exchange": round(t * 1e6, 2),
+                          "bytes_moved": 3 * n * (3 * 8 + 2 * 4)} if fusedp else None}
+    if cpu_seconds:
+        gpu_buf = send[0][:plan.send[0]["size"]].cpu().numpy()
+        out["cpu_baseline"] = cpu_baseline_config4(cpu_seconds, gpu_buf)
+    del co, bis, fields, interiors, send, recv, wv
+    torch.cuda.empty_cache()
+    return out
 
 
-def bench_config5(torch, dev, _ghx, levels):
-    """BASELINE config 5 shape on one GPU: 10M cells, 5 % halo, 7 peers, random lids (seed
-    20260715), levels_first fp64: fused gather of all send lists + fused scatter of all recv
-    lists (unstructured plans)."""
+def config5_patterns(world=8, cells=None):
+    """BASELINE config 5's domains for `world` ranks (tools/config5_gen.cpp: gids rank*10^7 + i,
+    5 % halo from the other ranks, mt19937_64 seed 20260715, permuted storage) and every rank's
+    product make_pattern<unstructured>, the ranks emulated as threads of this process
+    (ghex_amd.context.LoopbackWorld: each passes only its own domain; reduced halos travel).
+    Returns ([(gids, outer, send lid arrays, recv lid arrays)] per rank, setup seconds)."""
+    from ghex_amd import unstructured as U
+    from ghex_amd.context import LoopbackWorld
+    from tools import config5 as C5
+    cells = C5.CELLS if cells is None else cells
+
+    def rank_fn(ctx):
+        r = ctx.rank()
+        gids, outer = C5.generate(r, world, cells)
+        t0 = time.perf_counter()
+        dd = U.DomainDescriptor(r, gids, outer)
+        pc = U.make_pattern(ctx, U.HaloGenerator(), [dd])
+        t = time.perf_counter() - t0
+        return gids, outer, pc.lid_arrays(0, 0), pc.lid_arrays(0, 1), t
+
+    t0 = time.perf_counter()
+    res = LoopbackWorld(world).run(rank_fn)
+    return [r[:4] for r in res], time.perf_counter() - t0, max(r[4] for r in res)
+
+
+def bench_config5(torch, dev, _ghx, levels, pats, cpu_seconds=None):
+    """BASELINE config 5 on one GPU as rank 0 of 8: rank 0's send and receive lid lists from
+    the product pattern (config5_patterns), levels_first fp64, value(gid, level) = gid*100 +
+    level. Timed: one fused gather launch over the 7 send lists + one fused scatter launch over
+    the 7 receive lists (hipGraph of 10). `verified`: that timed graph replayed once on send
+    buffers set to 0xFF, outer cells reset to -1 and receive buffers holding what each peer's
+    own send list packs (its gids' values): every send-buffer value and every cell checked.
+    cpu_baseline: the oracle's data_descriptor<cpu> get/set (cpu_seconds None: skipped)."""
     import ctypes
     import numpy as np
-    rng = np.random.default_rng(20260715)
-    n = 10_000_000
-    nh = n // 20
-    send = rng.choice(n, size=nh, replace=False)
-    recv = rng.permutation(n)[:nh]
-    cuts = np.sort(rng.choice(np.arange(1, nh), size=6, replace=False))
-    sl, rl = np.split(send, cuts), np.split(recv, cuts)
-    vals = torch.randn(n * levels, dtype=torch.float64, device=dev)
+    gids, outer, sends, recvs = pats[0]
+    n = gids.size
+    host = (gids.astype(np.float64)[:, None] * 100.0 +
+            np.arange(levels, dtype=np.float64)[None, :])
+    want = torch.from_numpy(host).to(dev)  # (n, levels): levels fastest
+    vals = want.clone()
+    out_t = torch.from_numpy(outer).to(dev)
+    # what each peer packs for rank 0 (its send list with the same tag), checked to be the gids
+    # of rank 0's receive list: the two ends of every message agree
+    peer_bytes = []
+    for rid, rr, tag, lids in recvs:
+        pg, _, psend, _ = pats[rr]
+        plids = next(l for (i, q, tg, l) in psend if q == 0 and tg == tag)
+        if not np.array_equal(pg[plids], gids[lids]):
+            raise RuntimeError(f"config5 pattern: rank {rr}'s send list to 0 (tag {tag}) does "
+                               "not carry rank 0's receive gids")
+        peer_bytes.append(np.ascontiguousarray(host[lids]).view(np.uint8).reshape(-1))
 
     def plan(lists, direction):
         ents, keep = [], []
-        for k, l in enumerate(lists):
+        for k, (_, _, _, l) in enumerate(lists):
             e = _ghx.UPackEntry()
             e.data.elem_size, e.data.levels, e.data.levels_first = 8, levels, 1
             e.data.index_stride, e.data.level_stride = levels, 1
@@ -1563,23 +1667,53 @@ def bench_config5(torch, dev, _ghx, levels):
                   ctypes.byref(h))
         return h
 
-    hp, hu = plan(sl, 0), plan(rl, 1)
-    bufs = [torch.empty(len(l) * levels * 8, dtype=torch.uint8, device=dev) for l in sl]
+    hp, hu = plan(sends, 0), plan(recvs, 1)
+    sbufs = [torch.empty(len(l) * levels * 8, dtype=torch.uint8, device=dev) for *_, l in sends]
+    rbufs = [torch.from_numpy(b).to(dev) for b in peer_bytes]
     fp = _ghx.ptr_array([vals.data_ptr()])
-    bp = _ghx.ptr_array([b.data_ptr() for b in bufs])
+    sp = _ghx.ptr_array([b.data_ptr() for b in sbufs])
+    rp = _ghx.ptr_array([b.data_ptr() for b in rbufs])
     L = _ghx.lib()
 
     def step(s):
-        L.ghx_uplan_execute(hp, fp, 1, bp, len(bufs), s)
-        L.ghx_uplan_execute(hu, fp, 1, bp, len(bufs), s)
-    t = _time_graph(torch, dev, step)
+        _ghx.check(L.ghx_uplan_execute(hp, fp, 1, sp, len(sbufs), s), "uplan pack")
+        _ghx.check(L.ghx_uplan_execute(hu, fp, 1, rp, len(rbufs), s), "uplan unpack")
+    keep = {}
+    t = _time_graph(torch, dev, step, keep=keep)
+    # verify the timed graph
+    vals[out_t] = -1.0
+    for b in sbufs:
+        b.fill_(0xFF)
+    torch.cuda.synchronize(dev)
+    keep["graph"].replay()
+    torch.cuda.synchronize(dev)
+    bad = int((vals != want).sum().item())
+    for (_, _, _, l), b in zip(sends, sbufs):
+        exp = torch.from_numpy(np.ascontiguousarray(host[l])).to(dev).view(-1)
+        bad += int((b.view(torch.float64) != exp).sum().item())
+    del keep
+    n_send = sum(len(l) for *_, l in sends)
+    n_recv = sum(len(l) for *_, l in recvs)
+    nbytes = 2 * (n_send + n_recv) * levels * 8
+    res = {"GBps": round(nbytes / t / 1e9, 1), "frac": round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4),
+           "us_per_exchange": round(t * 1e6, 2),
+           "bytes_per_exchange": nbytes, "cells": int(n - outer.size), "halo_cells": n_recv,
+           "send_cells": n_send, "peers": len(sends), "levels": levels,
+           "index_bytes_per_exchange": (n_send + n_recv) * 4,
+           "verified": bad == 0,
+           "verified_what": "the timed hipGraph (10 x (gather + scatter)) replayed once: send "
+                            "buffers set to 0xFF, outer cells to -1, receive buffers holding each "
+                            "peer's packed send list; every send value and every cell checked",
+           "inputs": "rank 0 of 8 (tools/config5_gen.cpp), lists from the product's "
+                     "make_pattern<unstructured> with the 8 ranks as threads"}
+    if cpu_seconds:
+        res["cpu_baseline"] = cpu_baseline_config5(cpu_seconds, host, sends, recvs, peer_bytes,
+                                                   [b.cpu().numpy() for b in sbufs], levels)
     L.ghx_uplan_destroy(hp)
     L.ghx_uplan_destroy(hu)
-    nbytes = 4 * nh * levels * 8
-    return {"GBps": round(nbytes / t / 1e9, 1), "frac": round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4),
-            "us_per_exchange": round(t * 1e6, 2),
-            "bytes_per_exchange": nbytes, "cells": n, "halo_cells": nh, "peers": 7,
-            "index_bytes_per_exchange": 2 * nh * 4}
+    del vals, want, sbufs, rbufs
+    torch.cuda.empty_cache()
+    return res
 
 
 def _cpu_info():
@@ -1785,6 +1919,112 @@ def cpu_baseline_ranks(N, Hw, seconds, orc, nbytes, send, recv):
                       f"x{min(its)}-{max(its)} in {slowest:.1f} s, one thread each "
                       f"(oracle/ghex_oracle.c); median_of_25 = BASELINE.md §4 per rank, the "
                       f"slowest rank's median"}
+
+
+def _pinned_loop(one_pass, seconds):
+    """Run one_pass in a thread pinned to the first core of the affinity set until >= 25 passes
+    AND >= `seconds`; returns (per-pass times, total seconds, pinned core or None)."""
+    import threading
+    _, _, share = _cpu_info()
+    res = {}
+
+    def body():
+        res["pinned"] = _pin(share[0])
+        one_pass()  # warm (page-faults the buffers)
+        times = []
+        t0 = time.perf_counter()
+        while True:
+            a = time.perf_counter()
+            one_pass()
+            b = time.perf_counter()
+            times.append(b - a)
+            if b - t0 >= seconds and len(times) >= 25:
+                res["times"], res["dt"] = times, b - t0
+                return
+    th = threading.Thread(target=body)
+    th.start()
+    th.join()
+    return res["times"], res["dt"], (share[0] if res["pinned"] else None)
+
+
+def cpu_baseline_config4(seconds, gpu_buf):
+    """Config 4's CPU path: the oracle's single-thread restatement of the reference serializer
+    (serialization<cpu>::pack_batch/unpack_batch, include/ghex/structured/pack_kernels.hpp:62-158)
+    packing and unpacking all five fields of the one message (communication_object::allocate's
+    layout, oracle.plan_buffers), pinned to one core. `matches_gpu`: its packed message equals
+    the GPU's (the timed graph's) on every field byte."""
+    import numpy as np
+    from oracle import oracle as orc
+    model, nproc, share = _cpu_info()
+    N, H = 256, 3
+    E = N + 2 * H
+    dom = orc.RegularDomain(0, (0, 0, 0), (N - 1,) * 3)
+    pat = orc.regular_make_pattern([[dom]], (0, 0, 0), (N - 1,) * 3, (H,) * 6, (1, 1, 1))[0][0]
+    val = np.arange(N ** 3, dtype=np.float64).reshape(N, N, N)
+    specs = []
+    for k, t in enumerate(CONFIG4_TYPES):
+        dt = np.float64 if t == "f64" else np.float32
+        a = np.full((E, E, E), -1, dtype=dt)
+        a[H:H + N, H:H + N, H:H + N] = ((val + k) % (1 << 23)).astype(dt)
+        specs.append(orc.FieldSpec(a, a.itemsize, (2, 1, 0), (H,) * 3, (E,) * 3))
+    del val
+    items = [(k, 0, pat, sp.elem, sp.elem, 1, 0) for k, sp in enumerate(specs)]
+    (sb,) = orc.plan_buffers(items, receive=False).values()
+    (rb,) = orc.plan_buffers(items, receive=True).values()
+    buf = np.zeros(sb.size, np.uint8)
+
+    def one_pass():
+        for pf in sb.fields:
+            orc.structured_pack(specs[pf.field_index], buf, pf.boxes, pf.offset)
+        for pf in rb.fields:
+            orc.structured_unpack(specs[pf.field_index], buf, pf.boxes, pf.offset)
+    one_pass()
+    n = E ** 3 - N ** 3
+    same = buf.size == gpu_buf.size and all(
+        np.array_equal(buf[pf.offset:pf.offset + n * specs[pf.field_index].elem],
+                       gpu_buf[pf.offset:pf.offset + n * specs[pf.field_index].elem])
+        for pf in sb.fields)
+    times, dt, core = _pinned_loop(one_pass, seconds)
+    nbytes = 4 * n * (3 * 8 + 2 * 4)
+    med = _median_of_25(times)
+    return {"value": round(nbytes * len(times) / dt / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "port", "cpu_model": model, "nproc": nproc, "pinned_core": core,
+            "median_of_25_GBps": round(nbytes / med / 1e9, 3), "matches_gpu": bool(same),
+            "sample": f"the whole config-4 exchange (5 fields 256^3, H=3, one message) pack+"
+                      f"unpack x{len(times)} in {dt:.1f} s, 1 thread (oracle/ghex_oracle.c "
+                      f"row-memcpy restatement)"}
+
+
+def cpu_baseline_config5(seconds, host, sends, recvs, peer_bytes, gpu_sbufs, levels):
+    """Config 5's CPU path: the oracle's restatement of data_descriptor<cpu>::get/set
+    (include/ghex/unstructured/user_concepts.hpp:385-440: one memcpy per value) over rank 0's
+    7 send and 7 receive lists, pinned to one core. `matches_gpu`: every packed send buffer
+    equals the GPU's (the timed graph's), bit for bit."""
+    import numpy as np
+    from oracle import oracle as orc
+    model, nproc, share = _cpu_info()
+    vals = np.ascontiguousarray(host).reshape(-1).copy()
+    sb = [np.zeros(len(l) * levels * 8, np.uint8) for *_, l in sends]
+    sl = [np.ascontiguousarray(l, dtype=np.int64) for *_, l in sends]
+    rl = [np.ascontiguousarray(l, dtype=np.int64) for *_, l in recvs]
+
+    def one_pass():
+        for l, b in zip(sl, sb):
+            orc.unstructured_get(vals, b, 8, l, levels, True, levels, 1)
+        for l, b in zip(rl, peer_bytes):
+            orc.unstructured_set(vals, b, 8, l, levels, True, levels, 1)
+    one_pass()
+    same = all(np.array_equal(a, b) for a, b in zip(sb, gpu_sbufs)) and \
+        np.array_equal(vals, np.ascontiguousarray(host).reshape(-1))
+    times, dt, core = _pinned_loop(one_pass, seconds)
+    n_send, n_recv = sum(map(len, sl)), sum(map(len, rl))
+    nbytes = 2 * (n_send + n_recv) * levels * 8
+    med = _median_of_25(times)
+    return {"value": round(nbytes * len(times) / dt / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "port", "cpu_model": model, "nproc": nproc, "pinned_core": core,
+            "median_of_25_GBps": round(nbytes / med / 1e9, 3), "matches_gpu": bool(same),
+            "sample": f"rank 0's 7 gathers + 7 scatters (levels={levels}) x{len(times)} in "
+                      f"{dt:.1f} s, 1 thread (oracle/ghex_oracle.c get/set restatement)"}
 
 
 if __name__ == "__main__":

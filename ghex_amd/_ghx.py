@@ -73,9 +73,18 @@ _SIGS = {
                                            P(c_i32), P(c_i32), c_i32, P(c_vp)]),
     "ghx_staged_pattern_create": (c_i32, [c_i32, P(RegularDomain), c_i32, P(c_i32), P(c_i32),
                                           P(c_i32), P(c_i32), P(c_i32), c_i32, P(c_vp)]),
-    "ghx_unstructured_pattern_create": (c_i32, [c_i32, P(c_i32), P(c_i32), P(c_i64), P(c_i64),
-                                                P(c_i64), P(c_i64), P(c_i64), P(c_i64), c_i32,
-                                                P(c_vp)]),
+    "ghx_udomain_create": (c_i32, [c_i32, P(c_i64), c_i64, P(c_i64), c_i64, P(c_vp)]),
+    "ghx_udomain_destroy": (c_i32, [c_vp]),
+    "ghx_udomain_info": (c_i32, [c_vp, P(c_i32), P(c_i64), P(c_i64), P(c_i64)]),
+    "ghx_udomain_halo": (c_i32, [c_vp, P(c_i64), c_i64, P(c_i64), c_i64, P(c_i64)]),
+    "ghx_upattern_create": (c_i32, [P(c_vp), c_i32, c_i32, c_i32, c_i32, P(c_vp)]),
+    "ghx_upattern_add_halos": (c_i32, [c_vp, c_i32, c_i32, P(c_i32), P(c_i64), P(c_i64),
+                                       P(c_i64)]),
+    "ghx_upattern_record": (c_i32, [c_vp, c_i64, P(c_i32), P(c_i32), P(c_i32), P(c_i32),
+                                    P(c_i64), P(P(c_i64))]),
+    "ghx_upattern_add_recv": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, P(c_i64), c_i64]),
+    "ghx_upattern_finish": (c_i32, [c_vp, P(c_vp)]),
+    "ghx_upattern_destroy": (c_i32, [c_vp]),
     "ghx_pattern_destroy": (c_i32, [c_vp]),
     "ghx_pattern_filter": (c_i32, [c_vp, P(c_i32), c_i32, c_i32, P(c_vp)]),
     "ghx_pattern_num_domains": (c_i32, [c_vp, P(c_i32)]),
@@ -186,3 +195,8 @@ def i32_array(vals):
 
 def i64_array(vals):
     return (c_i64 * max(1, len(vals)))(*vals)
+
+
+def i64_ptr(a):
+    """ctypes int64* into a C-contiguous numpy int64 array (kept alive by the caller)."""
+    return a.ctypes.data_as(ctypes.POINTER(c_i64))

@@ -44,6 +44,68 @@ class Context:
         self._dist.all_gather_object(out, obj, group=self.group)
         return out
 
+    def _collective_device(self):
+        import torch
+        if self._dist.get_backend(self.group) == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def all_gather_array(self, arr):
+        """Setup-time all-gather of one int64 array per rank (sizes may differ), as tensors (no
+        pickling): the reduced halos of make_pattern<unstructured> (the reference moves them
+        around its distributed_for_each ring, include/ghex/mpi/communicator.hpp:233-345)."""
+        import numpy as np
+        arr = np.ascontiguousarray(arr, dtype=np.int64)
+        if self._dist is None or self._size == 1:
+            return [arr]
+        import torch
+        dev = self._collective_device()
+        n = torch.tensor([arr.size], dtype=torch.int64, device=dev)
+        ns = [torch.empty_like(n) for _ in range(self._size)]
+        self._dist.all_gather(ns, n, group=self.group)
+        sizes = [int(x.item()) for x in ns]
+        m = max(1, max(sizes))
+        t = torch.zeros(m, dtype=torch.int64, device=dev)
+        t[:arr.size] = torch.from_numpy(arr).to(dev)
+        outs = [torch.empty(m, dtype=torch.int64, device=dev) for _ in range(self._size)]
+        self._dist.all_gather(outs, t, group=self.group)
+        return [o[:k].cpu().numpy() for o, k in zip(outs, sizes)]
+
+    def exchange_arrays(self, sends, recvs):
+        """Setup-time point-to-point: sends = [(dst rank, int64 array)], recvs = [(src rank,
+        length)]; returns the received arrays in `recvs` order. Messages of one (src, dst) pair
+        are matched in order (the reference's isend/recv of gid lists,
+        include/ghex/unstructured/pattern.hpp:321, 352)."""
+        import numpy as np
+        me = self.rank()
+        out = [None] * len(recvs)
+        own = [np.ascontiguousarray(a, dtype=np.int64) for d, a in sends if d == me]
+        for k, (src, n) in enumerate(recvs):
+            if src == me:
+                out[k] = own.pop(0)
+        if self._dist is None or self._size == 1:
+            return out
+        import torch
+        dist, dev = self._dist, self._collective_device()
+        ops, keep = [], []
+        for d, a in sends:
+            if d != me:
+                t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).to(dev)
+                keep.append(t)
+                ops.append(dist.P2POp(dist.isend, t, self.global_rank(d), self.group))
+        slots = []
+        for k, (src, n) in enumerate(recvs):
+            if src != me:
+                t = torch.empty(int(n), dtype=torch.int64, device=dev)
+                slots.append((k, t))
+                ops.append(dist.P2POp(dist.irecv, t, self.global_rank(src), self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for k, t in slots:
+            out[k] = t.cpu().numpy()
+        return out
+
     def pair_communicators(self, peers, order):
         """One 2-rank RCCL communicator per peer (a 1-rank one for this rank itself), created at
         the first request (setup time, collective over the context: every rank reaches it
@@ -107,3 +169,95 @@ class Context:
 def make_context(comm=None, thread_safe: bool = False) -> Context:
     """make_context(comm, thread_safe) — comm is a torch.distributed group (None = WORLD)."""
     return Context(comm)
+
+
+class LoopbackWorld:
+    """Several ranks as threads of one process, for the setup collectives only (patterns): the
+    Python side of the C++ loopback_hub (include/ghex_amd/transport.hpp). run(fn) calls fn(ctx) on
+    one thread per rank and returns the results in rank order; the native work inside
+    (ghx_udomain_*, ghx_upattern_*) releases the GIL, so the ranks' setups run in parallel."""
+
+    def __init__(self, n: int):
+        import threading
+        if n < 1:
+            raise ValueError("LoopbackWorld needs at least one rank")
+        self.n = n
+        self._bar = threading.Barrier(n)
+        self._slots = [None] * n
+        self._mail = {}
+        self._lock = threading.Lock()
+
+    def context(self, rank: int) -> "LoopbackContext":
+        return LoopbackContext(self, rank)
+
+    def run(self, fn):
+        import threading
+        res, err = [None] * self.n, []
+
+        def body(r):
+            try:
+                res[r] = fn(self.context(r))
+            except BaseException as e:  # noqa: BLE001 - re-raised below
+                with self._lock:
+                    err.append((r, e))
+                self._bar.abort()
+
+        ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(self.n)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if err:
+            import threading as _t
+            first = sorted(((r, e) for r, e in err
+                            if not isinstance(e, _t.BrokenBarrierError)), key=lambda x: x[0])
+            raise (first or err)[0][1]
+        return res
+
+
+class LoopbackContext:
+    """One rank of a LoopbackWorld (rank, size and the setup collectives of Context)."""
+
+    distributed = None
+    group = None
+
+    def __init__(self, world: LoopbackWorld, rank: int):
+        self._w, self._r = world, rank
+
+    def rank(self) -> int:
+        return self._r
+
+    def size(self) -> int:
+        return self._w.n
+
+    def global_rank(self, r: int) -> int:
+        return r
+
+    def all_gather_object(self, obj):
+        w = self._w
+        w._slots[self._r] = obj
+        w._bar.wait()
+        out = list(w._slots)
+        w._bar.wait()
+        return out
+
+    def all_gather_array(self, arr):
+        import numpy as np
+        return self.all_gather_object(np.ascontiguousarray(arr, dtype=np.int64))
+
+    def exchange_arrays(self, sends, recvs):
+        import numpy as np
+        w, me = self._w, self._r
+        with w._lock:
+            for d, a in sends:
+                w._mail.setdefault((me, d), []).append(np.ascontiguousarray(a, dtype=np.int64))
+        w._bar.wait()
+        out = []
+        with w._lock:
+            for src, n in recvs:
+                a = w._mail[(src, me)].pop(0)
+                if a.size != n:
+                    raise RuntimeError(f"loopback exchange_arrays: {a.size} != {n} from {src}")
+                out.append(a)
+        w._bar.wait()
+        return out

@@ -17,10 +17,6 @@
 #include "ghx_pattern.hpp"
 #include "ghx_plan.hpp"
 
-struct ghx_pattern : ghx::pattern_set
-{
-};
-
 namespace ghx
 {
 namespace
@@ -792,28 +788,6 @@ int ghx_staged_pattern_create(int32_t dim, const ghx_regular_domain* domains, in
             static_cast<ghx::pattern_set&>(*ps.back()) = std::move(s);
         }
         for (int i = 0; i < dim; ++i) out[i] = ps[i].release();
-        return GHX_OK;
-    });
-}
-
-int ghx_unstructured_pattern_create(int32_t n_domains, const int32_t* domain_ids,
-                                    const int32_t* domain_ranks, const int64_t* gids,
-                                    const int64_t* gid_counts, const int64_t* outer_lids,
-                                    const int64_t* outer_counts, const int64_t* halo_gids,
-                                    const int64_t* halo_counts, int32_t my_rank,
-                                    ghx_pattern** out)
-{
-    return guarded([&] {
-        check_ptr(out, "out");
-        check_ptr(domain_ids, "domain_ids");
-        check_ptr(domain_ranks, "domain_ranks");
-        check_ptr(gid_counts, "gid_counts");
-        check_ptr(outer_counts, "outer_counts");
-        if (n_domains < 1) throw invalid("need at least one domain");
-        auto p = std::make_unique<ghx_pattern>();
-        unstructured_make_pattern(n_domains, domain_ids, domain_ranks, gids, gid_counts,
-                                  outer_lids, outer_counts, halo_gids, halo_counts, my_rank, *p);
-        *out = p.release();
         return GHX_OK;
     });
 }

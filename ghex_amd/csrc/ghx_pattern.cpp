@@ -196,158 +196,6 @@ int regular_make_pattern(int dim, const ghx_regular_domain* doms, int n, const i
 }
 
 // ---------------------------------------------------------------------------------------------
-// unstructured
-// ---------------------------------------------------------------------------------------------
-namespace
-{
-struct udomain
-{
-    int32_t id, rank;
-    std::vector<int64_t> gids;
-    std::unordered_map<int64_t, int64_t> inner;
-    // unordered_multimap equal_range order of libstdc++: reverse insertion order
-    std::unordered_map<int64_t, std::vector<int64_t>> outer;
-    std::vector<int64_t> outer_gids;
-
-    // domain_descriptor::make_outer_lids (user_concepts.hpp:88-113)
-    std::vector<int64_t> make_outer_lids(const std::vector<int64_t>& g) const
-    {
-        std::vector<int64_t> lids;
-        lids.reserve(g.size());
-        std::unordered_map<int64_t, size_t> count;
-        for (auto gid : g)
-        {
-            auto it = outer.find(gid);
-            if (it == outer.end()) continue;
-            auto c = count.find(gid);
-            if (c == count.end())
-            {
-                count.emplace(gid, 0);
-                lids.push_back(it->second[0]);
-            }
-            else
-            {
-                if (++c->second < it->second.size()) lids.push_back(it->second[c->second]);
-                else throw std::runtime_error("halo gid does not have an associated lid in the domain");
-            }
-        }
-        for (auto& kv : count)
-            if (kv.second + 1 != outer.find(kv.first)->second.size())
-                throw std::runtime_error("halo gid occurs not often enough");
-        return lids;
-    }
-};
-
-unsigned num_bits(unsigned n) { return n ? 1u + num_bits(n >> 1) : 1u; }
-}  // namespace
-
-int unstructured_make_pattern(int n, const int32_t* ids, const int32_t* ranks,
-                              const int64_t* gids, const int64_t* gid_counts,
-                              const int64_t* outer_lids, const int64_t* outer_counts,
-                              const int64_t* halo_gids, const int64_t* halo_counts, int my_rank,
-                              pattern_set& out)
-{
-    // domain_descriptor ctor (user_concepts.hpp:143-175)
-    std::vector<udomain> D(n);
-    int64_t go = 0, oo = 0;
-    for (int i = 0; i < n; ++i)
-    {
-        auto& d = D[i];
-        d.id = ids[i];
-        d.rank = ranks[i];
-        std::unordered_set<int64_t> outer_set;
-        for (int64_t k = 0; k < outer_counts[i]; ++k)
-            if (!outer_set.insert(outer_lids[oo + k]).second)
-                throw std::runtime_error("repeated outer (local) index");
-        oo += outer_counts[i];
-        for (int64_t lid = 0; lid < gid_counts[i]; ++lid)
-        {
-            const int64_t gid = gids[go + lid];
-            if (outer_set.count(lid))
-            {
-                auto& v = d.outer[gid];
-                v.insert(v.begin(), lid);
-                d.outer_gids.push_back(gid);
-            }
-            else if (!d.inner.emplace(gid, lid).second)
-                throw std::runtime_error("repeated inner (global) index");
-            d.gids.push_back(gid);
-        }
-        go += gid_counts[i];
-    }
-    int world = 0;
-    for (auto& d : D) world = std::max(world, d.rank + 1);
-    std::vector<std::vector<int>> by_rank(world);
-    for (int i = 0; i < n; ++i) by_rank[D[i].rank].push_back(i);
-    unsigned max_num_domains = 0;
-    int32_t max_domain_id = 0;
-    for (auto& v : by_rank) max_num_domains = std::max<unsigned>(max_num_domains, v.size());
-    for (auto& d : D) max_domain_id = std::max(max_domain_id, d.id);
-    const unsigned shift = num_bits(max_num_domains);
-    auto make_tag = [shift](unsigned src_local_idx, int32_t tgt) {
-        return int32_t((src_local_idx << shift) | unsigned(tgt));
-    };
-    // halo gids of every domain, in halo (generator) order
-    std::vector<std::vector<int64_t>> halo(n);
-    int64_t ho = 0;
-    for (int i = 0; i < n; ++i)
-    {
-        std::vector<int64_t> hg;
-        if (halo_gids && halo_counts && halo_counts[i] >= 0)
-        {
-            hg.assign(halo_gids + ho, halo_gids + ho + halo_counts[i]);
-            ho += halo_counts[i];
-        }
-        else hg = D[i].outer_gids;
-        for (auto lid : D[i].make_outer_lids(hg)) halo[i].push_back(D[i].gids[lid]);
-    }
-    // send halos of domain s (local index i on its rank) towards every domain o (:272-330);
-    // recv halos = make_outer_lids of the same gid sequence on the receiver (:337-365)
-    out = pattern_set{};
-    out.kind = 1;
-    out.dim = 1;
-    out.max_tag = make_tag(max_num_domains, max_domain_id);
-    out.my_rank = my_rank;
-    if (my_rank >= world) return GHX_OK;
-    for (size_t li = 0; li < by_rank[my_rank].size(); ++li)
-    {
-        const int a = by_rank[my_rank][li];
-        const auto& d = D[a];
-        domain_pattern p;
-        p.id = d.id;
-        std::map<std::pair<int32_t, int32_t>, halo_entry> send, recv;
-        for (int o = 0; o < n; ++o)
-        {
-            halo_entry e;
-            for (auto g : halo[o])
-            {
-                auto it = d.inner.find(g);
-                if (it != d.inner.end()) e.lids.push_back(it->second);
-            }
-            if (e.lids.empty()) continue;
-            e.key = {D[o].id, D[o].rank, make_tag(unsigned(li), D[o].id)};
-            send.emplace(std::make_pair(e.key.remote_rank, e.key.tag), std::move(e));
-        }
-        for (int src = 0; src < world; ++src)
-            for (size_t sj = 0; sj < by_rank[src].size(); ++sj)
-            {
-                const auto& s = D[by_rank[src][sj]];
-                std::vector<int64_t> g;
-                for (auto x : halo[a])
-                    if (s.inner.count(x)) g.push_back(x);
-                if (g.empty()) continue;
-                halo_entry e;
-                e.key = {s.id, s.rank, make_tag(unsigned(sj), d.id)};
-                e.lids = d.make_outer_lids(g);
-                recv.emplace(std::make_pair(e.key.remote_rank, e.key.tag), std::move(e));
-            }
-        for (auto& kv : send) p.send.push_back(std::move(kv.second));
-        for (auto& kv : recv) p.recv.push_back(std::move(kv.second));
-        out.doms.push_back(std::move(p));
-    }
-    return GHX_OK;
-}
-// ---------------------------------------------------------------------------------------------
 // staged (dimension-by-dimension) patterns
 // ---------------------------------------------------------------------------------------------
 // make_staged_pattern (include/ghex/structured/regular/make_pattern.hpp:47-250): one pattern per

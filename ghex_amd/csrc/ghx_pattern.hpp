@@ -63,9 +63,9 @@ void staged_make_pattern(int dim, const ghx_regular_domain* doms, int n, const i
                          const int32_t* gfirst, const int32_t* glast, const int32_t* halos,
                          const int32_t* periodic, int my_rank, std::vector<pattern_set>& out);
 
-int unstructured_make_pattern(int n, const int32_t* ids, const int32_t* ranks,
-                              const int64_t* gids, const int64_t* gid_counts,
-                              const int64_t* outer_lids, const int64_t* outer_counts,
-                              const int64_t* halo_gids, const int64_t* halo_counts, int my_rank,
-                              pattern_set& out);
 }  // namespace ghx
+
+// the opaque C-ABI pattern handle (include/ghx.h)
+struct ghx_pattern : ghx::pattern_set
+{
+};

@@ -87,6 +87,20 @@ class PatternContainer:
             out.append((rid, rr, tag, sp))
         return out
 
+    def lid_arrays(self, local_index: int, direction: int):
+        """Unstructured: halos(local_index, direction) with each lid list as an int64 numpy
+        array (no Python list of ints)."""
+        import numpy as np
+        if self.kind == "structured":
+            raise TypeError("lid_arrays is for unstructured patterns")
+        out = []
+        for k, rid, rr, tag, ns, ne in self._keys(local_index, direction):
+            arr = np.empty(max(1, ne), dtype=np.int64)
+            _ghx.call("ghx_pattern_key_lids", self._h, local_index, direction, k,
+                      _ghx.i64_ptr(arr), ne)
+            out.append((rid, rr, tag, arr[:ne]))
+        return out
+
     def send_halos(self, local_index: int = 0):
         return self.halos(local_index, 0)
 

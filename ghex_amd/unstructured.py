@@ -3,7 +3,7 @@ on the MI355X-native path: index-list gather/scatter halos."""
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Sequence
+from typing import Sequence
 
 from . import _ghx
 from .communication_object import CommunicationObject
@@ -17,40 +17,56 @@ def make_communication_object(context, **options) -> CommunicationObject:
 class DomainDescriptor:
     """unstructured::domain_descriptor(id, gids, outer_lids)
     (include/ghex/unstructured/user_concepts.hpp:143-175): all global ids in storage order and
-    the local ids of the outer (halo) cells."""
+    the local ids of the outer (halo) cells. The gid -> lid maps live in libghx (ghx_udomain,
+    flat hash tables built once); gids and outer lids are kept here as int64 numpy arrays."""
 
-    def __init__(self, index: int, indices: Sequence[int], halo_indices: Sequence[int]):
+    def __init__(self, index: int, indices, halo_indices):
+        import numpy as np
         self._id = int(index)
-        self.gids = [int(g) for g in indices]
-        self.outer_lids = [int(l) for l in halo_indices]
-        if len(set(self.outer_lids)) != len(self.outer_lids):
-            raise RuntimeError("repeated outer (local) index")
-        outer = set(self.outer_lids)
-        inner = {}
-        for lid, gid in enumerate(self.gids):
-            if lid in outer:
-                continue
-            if gid in inner:
-                raise RuntimeError("repeated inner (global) index")
-            inner[gid] = lid
-        self._inner = inner
+        self.gids = np.ascontiguousarray(indices, dtype=np.int64).reshape(-1)
+        self.outer_lids = np.ascontiguousarray(halo_indices, dtype=np.int64).reshape(-1)
+        h = ctypes.c_void_p()
+        _ghx.call("ghx_udomain_create", self._id, _ghx.i64_ptr(self.gids), self.gids.size,
+                  _ghx.i64_ptr(self.outer_lids), self.outer_lids.size, ctypes.byref(h))
+        self._h = h
+        inner = ctypes.c_int64()
+        _ghx.call("ghx_udomain_info", h, None, None, ctypes.byref(inner), None)
+        self._inner_size = inner.value
+
+    def __del__(self):
+        h = self.__dict__.get("_h")
+        if h is not None and h.value and _ghx is not None and _ghx._lib is not None:
+            _ghx._lib.ghx_udomain_destroy(h)
+            self._h = None
 
     def domain_id(self) -> int:
         return self._id
 
     def size(self) -> int:
-        return len(self.gids)
+        return int(self.gids.size)
 
     def inner_size(self) -> int:
-        return len(self._inner)
+        return self._inner_size
+
+    def halo_gids(self, halo_gen: "HaloGenerator"):
+        """The reduced halo: gids of halo_gen(domain)'s local indices (pattern.hpp:247-254)."""
+        import numpy as np
+        g = halo_gen.gids
+        cap = self.outer_lids.size if g is None else g.size
+        out = np.empty(max(1, cap), dtype=np.int64)
+        n = ctypes.c_int64()
+        _ghx.call("ghx_udomain_halo", self._h, None if g is None else _ghx.i64_ptr(g),
+                  -1 if g is None else g.size, _ghx.i64_ptr(out), cap, ctypes.byref(n))
+        return out[:n.value]
 
 
 class HaloGenerator:
     """unstructured::halo_generator (user_concepts.hpp:234-253): all outer gids (default) or
     an explicit halo gid list."""
 
-    def __init__(self, gids: Optional[Sequence[int]] = None):
-        self.gids = None if gids is None else [int(g) for g in gids]
+    def __init__(self, gids=None):
+        import numpy as np
+        self.gids = None if gids is None else np.ascontiguousarray(gids, dtype=np.int64).reshape(-1)
 
     @classmethod
     def from_gids(cls, gids):
@@ -58,29 +74,63 @@ class HaloGenerator:
 
 
 def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[DomainDescriptor]):
-    """make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370)."""
-    mine = [(d.domain_id(), d.gids, d.outer_lids, halo_gen.gids) for d in domain_range]
-    gathered = context.all_gather_object(mine)
-    ids, ranks, gids, gc, outer, oc, hg, hc = [], [], [], [], [], [], [], []
-    for r, lst in enumerate(gathered):
-        for (i, g, o, h) in lst:
-            ids.append(i)
-            ranks.append(r)
-            gids += g
-            gc.append(len(g))
-            outer += o
-            oc.append(len(o))
-            if h is None:
-                hc.append(-1)
-            else:
-                hg += h
-                hc.append(len(h))
-    p = ctypes.c_void_p()
-    _ghx.call("ghx_unstructured_pattern_create", len(ids), _ghx.i32_array(ids),
-              _ghx.i32_array(ranks), _ghx.i64_array(gids), _ghx.i64_array(gc),
-              _ghx.i64_array(outer), _ghx.i64_array(oc), _ghx.i64_array(hg),
-              _ghx.i64_array(hc), context.rank(), ctypes.byref(p))
-    return PatternContainer(p.value, context, domain_range, "unstructured", 1)
+    """make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370), the
+    reference's reduced-halo algorithm: this rank passes only its own domains; the ranks
+    exchange their domains' halo gids (never their full gid lists), each rank resolves every
+    halo against its own inner gids (its send halos) and ships the gids it found back to the
+    halo's owner, which turns them into outer local ids (its receive halos). Collectives:
+    `context.all_gather_object` (ids, record metadata), `context.all_gather_array` (reduced
+    halos), `context.exchange_arrays` (gid lists, point to point)."""
+    import numpy as np
+    doms = list(domain_range)
+    if not doms:
+        raise ValueError("make_pattern needs at least one local domain")
+    me = context.rank()
+    ids = [d.domain_id() for d in doms]
+    # tags from the global max domain id and max domains per rank (:218-233)
+    meta = context.all_gather_object((max(ids), len(ids)))
+    max_id = max(m[0] for m in meta)
+    max_n = max(m[1] for m in meta)
+    handles = (ctypes.c_void_p * len(doms))(*[d._h.value for d in doms])
+    b = ctypes.c_void_p()
+    _ghx.call("ghx_upattern_create", handles, len(doms), me, max_n, max_id, ctypes.byref(b))
+    try:
+        # reduced halos of my domains: [n, ids..., sizes..., gids...] (:243-254)
+        halos = [d.halo_gids(halo_gen) for d in doms]
+        payload = np.concatenate([np.array([len(doms)], np.int64), np.array(ids, np.int64),
+                                  np.array([h.size for h in halos], np.int64)] + halos)
+        n_rec = ctypes.c_int64()
+        # every rank's reduced halos against my inner gids -> send halos (:284-330)
+        for r, arr in enumerate(context.all_gather_array(payload)):
+            k = int(arr[0])
+            rid = np.ascontiguousarray(arr[1:1 + k], dtype=np.int32)
+            sizes = np.ascontiguousarray(arr[1 + k:1 + 2 * k])
+            gids = np.ascontiguousarray(arr[1 + 2 * k:])
+            _ghx.call("ghx_upattern_add_halos", b, r, k,
+                      rid.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _ghx.i64_ptr(sizes),
+                      _ghx.i64_ptr(gids), ctypes.byref(n_rec))
+        recs, sends = [], []
+        f = [ctypes.c_int32() for _ in range(4)]
+        n = ctypes.c_int64()
+        gp = ctypes.POINTER(ctypes.c_int64)()
+        for k in range(n_rec.value):
+            _ghx.call("ghx_upattern_record", b, k, *[ctypes.byref(x) for x in f],
+                      ctypes.byref(n), ctypes.byref(gp))
+            src_id, dst_id, dst_rank, tag = (x.value for x in f)
+            recs.append((src_id, dst_id, dst_rank, tag, n.value))
+            sends.append((dst_rank, np.ctypeslib.as_array(gp, shape=(n.value,)).copy()))
+        # the records addressed to me, then the gid lists point to point (:337-365)
+        every = context.all_gather_object(recs)
+        mine = [(src, rec) for src, rs in enumerate(every) for rec in rs if rec[2] == me]
+        got = context.exchange_arrays(sends, [(src, rec[4]) for src, rec in mine])
+        for (src, (src_id, dst_id, _, tag, cnt)), g in zip(mine, got):
+            g = np.ascontiguousarray(g, dtype=np.int64)
+            _ghx.call("ghx_upattern_add_recv", b, src, src_id, dst_id, tag, _ghx.i64_ptr(g), cnt)
+        p = ctypes.c_void_p()
+        _ghx.call("ghx_upattern_finish", b, ctypes.byref(p))
+    finally:
+        _ghx.lib().ghx_upattern_destroy(b)
+    return PatternContainer(p.value, context, doms, "unstructured", 1)
 
 
 class DataDescriptor:

@@ -221,11 +221,13 @@ inline pattern_container make_pattern(context& ctx, const halo_generator& hg,
 namespace unstructured
 {
 // unstructured::domain_descriptor (user_concepts.hpp:143-175): all global ids in storage order
-// and the local ids of the outer (halo) cells.
+// and the local ids of the outer (halo) cells; the gid -> lid maps are built once in libghx
+// (ghx_udomain_create).
 class domain_descriptor
 {
     int m_id;
     std::vector<std::int64_t> m_gids, m_outer;
+    std::shared_ptr<ghx_udomain> m_h;
 
   public:
     domain_descriptor(int id, std::vector<std::int64_t> gids, std::vector<std::int64_t> outer_lids)
@@ -233,11 +235,17 @@ class domain_descriptor
     , m_gids(std::move(gids))
     , m_outer(std::move(outer_lids))
     {
+        ghx_udomain* h = nullptr;
+        check_ghx(ghx_udomain_create(id, m_gids.data(), std::int64_t(m_gids.size()), m_outer.data(),
+                                     std::int64_t(m_outer.size()), &h),
+                  "ghx_udomain_create");
+        m_h.reset(h, [](ghx_udomain* q) { ghx_udomain_destroy(q); });
     }
     int domain_id() const { return m_id; }
     std::size_t size() const { return m_gids.size(); }
     const std::vector<std::int64_t>& gids() const { return m_gids; }
     const std::vector<std::int64_t>& outer_lids() const { return m_outer; }
+    const ghx_udomain* handle() const { return m_h.get(); }
 };
 
 // unstructured::halo_generator (user_concepts.hpp:234-253): every outer gid (default) or an
@@ -248,50 +256,119 @@ struct halo_generator
     std::vector<std::int64_t> gids;
 };
 
-// make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370)
+// make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370): the
+// reference's reduced-halo algorithm through the context's all_gather. Only halo gids travel:
+// (1) max domain id / count, (2) every rank's reduced halos, (3) the gid lists of the send
+// halos found in (2), which their receivers turn into outer lids.
 inline pattern_container make_pattern(context& ctx, const halo_generator& hg,
                                       const std::vector<domain_descriptor>& domains)
 {
+    if (domains.empty()) throw std::runtime_error("make_pattern needs at least one local domain");
+    auto& tr = ctx.get_transport();
+    const int me = ctx.rank();
+    std::int32_t max_id = 0;
+    for (const auto& d : domains) max_id = std::max<std::int32_t>(max_id, d.domain_id());
+    std::vector<char> meta;
+    detail::put(meta, max_id);
+    detail::put(meta, std::int32_t(domains.size()));
+    std::int32_t g_max_id = 0, g_max_n = 0;
+    for (const auto& m : tr.all_gather(meta))
+    {
+        std::size_t pos = 0;
+        g_max_id = std::max(g_max_id, detail::get<std::int32_t>(m, pos));
+        g_max_n = std::max(g_max_n, detail::get<std::int32_t>(m, pos));
+    }
+    std::vector<const ghx_udomain*> hs;
+    for (const auto& d : domains) hs.push_back(d.handle());
+    ghx_upattern* b = nullptr;
+    check_ghx(ghx_upattern_create(hs.data(), std::int32_t(hs.size()), me, g_max_n, g_max_id, &b),
+              "ghx_upattern_create");
+    std::unique_ptr<ghx_upattern, int (*)(ghx_upattern*)> guard(b, ghx_upattern_destroy);
+    // (2) reduced halos: [n][ids][sizes][gids...]
     std::vector<char> mine;
     detail::put(mine, std::int32_t(domains.size()));
+    std::vector<std::vector<std::int64_t>> halos;
     for (const auto& d : domains)
     {
+        const std::int64_t cap = hg.all_outer ? std::int64_t(d.outer_lids().size())
+                                              : std::int64_t(hg.gids.size());
+        std::vector<std::int64_t> h(std::size_t(std::max<std::int64_t>(cap, 1)));
+        std::int64_t n = 0;
+        check_ghx(ghx_udomain_halo(d.handle(), hg.all_outer ? nullptr : hg.gids.data(),
+                                   hg.all_outer ? -1 : std::int64_t(hg.gids.size()), h.data(), cap,
+                                   &n),
+                  "ghx_udomain_halo");
+        h.resize(std::size_t(n));
         detail::put(mine, std::int32_t(d.domain_id()));
-        detail::put(mine, std::int64_t(d.gids().size()));
-        for (auto g : d.gids()) detail::put(mine, g);
-        detail::put(mine, std::int64_t(d.outer_lids().size()));
-        for (auto l : d.outer_lids()) detail::put(mine, l);
-        detail::put(mine, std::int64_t(hg.all_outer ? -1 : std::int64_t(hg.gids.size())));
-        if (!hg.all_outer)
-            for (auto g : hg.gids) detail::put(mine, g);
+        detail::put(mine, n);
+        halos.push_back(std::move(h));
     }
-    const auto all = ctx.get_transport().all_gather(mine);
-    std::vector<std::int32_t> ids, ranks;
-    std::vector<std::int64_t> gids, gc, outer, oc, hgid, hc;
+    for (const auto& h : halos)
+    {
+        const char* p = reinterpret_cast<const char*>(h.data());
+        mine.insert(mine.end(), p, p + h.size() * sizeof(std::int64_t));
+    }
+    const auto all = tr.all_gather(mine);
+    std::int64_t n_rec = 0;
     for (std::size_t r = 0; r < all.size(); ++r)
     {
         std::size_t pos = 0;
         const auto n = detail::get<std::int32_t>(all[r], pos);
+        std::vector<std::int32_t> ids;
+        std::vector<std::int64_t> sizes, gids;
         for (std::int32_t i = 0; i < n; ++i)
         {
             ids.push_back(detail::get<std::int32_t>(all[r], pos));
-            ranks.push_back(std::int32_t(r));
-            const auto ng = detail::get<std::int64_t>(all[r], pos);
-            gc.push_back(ng);
-            for (std::int64_t k = 0; k < ng; ++k) gids.push_back(detail::get<std::int64_t>(all[r], pos));
-            const auto no = detail::get<std::int64_t>(all[r], pos);
-            oc.push_back(no);
-            for (std::int64_t k = 0; k < no; ++k) outer.push_back(detail::get<std::int64_t>(all[r], pos));
-            const auto nh = detail::get<std::int64_t>(all[r], pos);
-            hc.push_back(nh);
-            for (std::int64_t k = 0; k < nh; ++k) hgid.push_back(detail::get<std::int64_t>(all[r], pos));
+            sizes.push_back(detail::get<std::int64_t>(all[r], pos));
+        }
+        for (auto s : sizes)
+            for (std::int64_t k = 0; k < s; ++k) gids.push_back(detail::get<std::int64_t>(all[r], pos));
+        check_ghx(ghx_upattern_add_halos(b, std::int32_t(r), n, ids.data(), sizes.data(),
+                                         gids.data(), &n_rec),
+                  "ghx_upattern_add_halos");
+    }
+    // (3) the send halos' gid lists to their receivers
+    std::vector<char> recs;
+    detail::put(recs, n_rec);
+    for (std::int64_t k = 0; k < n_rec; ++k)
+    {
+        std::int32_t src_id, dst_id, dst_rank, tag;
+        std::int64_t n = 0;
+        const std::int64_t* g = nullptr;
+        check_ghx(ghx_upattern_record(b, k, &src_id, &dst_id, &dst_rank, &tag, &n, &g),
+                  "ghx_upattern_record");
+        for (auto v : {src_id, dst_id, dst_rank, tag}) detail::put(recs, v);
+        detail::put(recs, n);
+        const char* p = reinterpret_cast<const char*>(g);
+        recs.insert(recs.end(), p, p + std::size_t(n) * sizeof(std::int64_t));
+    }
+    const auto every = tr.all_gather(recs);
+    for (std::size_t r = 0; r < every.size(); ++r)
+    {
+        std::size_t pos = 0;
+        const auto n = detail::get<std::int64_t>(every[r], pos);
+        for (std::int64_t k = 0; k < n; ++k)
+        {
+            const auto src_id = detail::get<std::int32_t>(every[r], pos);
+            const auto dst_id = detail::get<std::int32_t>(every[r], pos);
+            const auto dst_rank = detail::get<std::int32_t>(every[r], pos);
+            const auto tag = detail::get<std::int32_t>(every[r], pos);
+            const auto cnt = detail::get<std::int64_t>(every[r], pos);
+            if (pos + std::size_t(cnt) * sizeof(std::int64_t) > every[r].size())
+                throw std::runtime_error("malformed all_gather payload");
+            if (dst_rank == me)
+            {
+                std::vector<std::int64_t> g(static_cast<std::size_t>(cnt));
+                std::memcpy(g.data(), every[r].data() + pos, g.size() * sizeof(std::int64_t));
+                check_ghx(ghx_upattern_add_recv(b, std::int32_t(r), src_id, dst_id, tag, g.data(),
+                                                cnt),
+                          "ghx_upattern_add_recv");
+            }
+            pos += std::size_t(cnt) * sizeof(std::int64_t);
         }
     }
     ghx_pattern* p = nullptr;
-    check_ghx(ghx_unstructured_pattern_create(std::int32_t(ids.size()), ids.data(), ranks.data(),
-                                              gids.data(), gc.data(), outer.data(), oc.data(),
-                                              hgid.data(), hc.data(), ctx.rank(), &p),
-              "ghx_unstructured_pattern_create");
+    check_ghx(ghx_upattern_finish(b, &p), "ghx_upattern_finish");
     return pattern_container(p);
 }
 }  // namespace unstructured

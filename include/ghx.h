@@ -249,16 +249,48 @@ int ghx_staged_pattern_create(int32_t dim, const ghx_regular_domain* domains, in
                               const int32_t* global_last, const int32_t* halos,
                               const int32_t* periodic, int32_t my_rank, ghx_pattern** out);
 
-/* make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370) for rank
- * `my_rank`. For every domain d of every rank: gids[d] (storage order), the outer (halo) local
- * ids, and optionally the halo generator's gid list (NULL/-1 = all outer gids,
- * user_concepts.hpp:244-252). Arrays are concatenated; *_count give per-domain lengths. */
-int ghx_unstructured_pattern_create(int32_t n_domains, const int32_t* domain_ids,
-                                    const int32_t* domain_ranks, const int64_t* gids,
-                                    const int64_t* gid_counts, const int64_t* outer_lids,
-                                    const int64_t* outer_counts, const int64_t* halo_gids,
-                                    const int64_t* halo_counts, int32_t my_rank,
-                                    ghx_pattern** out);
+/* unstructured::domain_descriptor(id, gids, outer lids) (include/ghex/unstructured/
+ * user_concepts.hpp:37-176): gids in storage order, the local ids of the outer (halo) cells.
+ * Builds the gid -> lid maps (flat hash tables) once; immutable afterwards (shareable between
+ * threads). Fails (GHX_ERR_PATTERN) on a repeated outer lid or a repeated inner gid, like the
+ * reference's constructor. */
+typedef struct ghx_udomain ghx_udomain;
+int ghx_udomain_create(int32_t id, const int64_t* gids, int64_t n_gids, const int64_t* outer_lids,
+                       int64_t n_outer, ghx_udomain** out);
+int ghx_udomain_destroy(ghx_udomain* d);
+int ghx_udomain_info(const ghx_udomain* d, int32_t* id, int64_t* size, int64_t* inner_size,
+                     int64_t* n_outer);
+/* halo_generator::operator() (user_concepts.hpp:234-256) as gids: the domain's reduced halo, i.e.
+ * the gids of make_outer_lids(gen_gids) (n_gen < 0: all outer gids in storage order). Writes
+ * *n_halo <= max(n_gen, n_outer) gids; cap must hold them. */
+int ghx_udomain_halo(const ghx_udomain* d, const int64_t* gen_gids, int64_t n_gen,
+                     int64_t* halo_gids, int64_t cap, int64_t* n_halo);
+
+/* make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370) for ONE rank,
+ * in the reference's three steps; the caller moves the bytes between ranks (only halo gids ever
+ * travel, never a rank's full gid list):
+ *   1. ghx_upattern_create with this rank's domains and the global max domain count per rank and
+ *      max domain id (the tag layout, :218-233);
+ *   2. ghx_upattern_add_halos once per rank r (this one included; any order) with r's domain ids
+ *      and reduced halos (ghx_udomain_halo, concatenated): creates this rank's send halos for
+ *      every halo gid that is an inner cell of one of its domains (:284-330) and a record per
+ *      (my domain, r's domain) pair whose gid list must reach rank dst_rank (ghx_upattern_record:
+ *      the pointer stays valid until ghx_upattern_destroy);
+ *   3. ghx_upattern_add_recv for every record addressed to this rank (src = the record's sender):
+ *      make_outer_lids -> receive halos (:337-365); then ghx_upattern_finish.
+ * Maps are keyed and ordered (rank, tag) as the reference's (pattern.hpp:105-110). */
+typedef struct ghx_upattern ghx_upattern;
+int ghx_upattern_create(const ghx_udomain* const* domains, int32_t n_domains, int32_t my_rank,
+                        int32_t max_num_domains, int32_t max_domain_id, ghx_upattern** out);
+int ghx_upattern_add_halos(ghx_upattern* b, int32_t rank, int32_t n_domains,
+                           const int32_t* domain_ids, const int64_t* halo_sizes,
+                           const int64_t* halo_gids, int64_t* n_records);
+int ghx_upattern_record(const ghx_upattern* b, int64_t k, int32_t* src_id, int32_t* dst_id,
+                        int32_t* dst_rank, int32_t* tag, int64_t* n_gids, const int64_t** gids);
+int ghx_upattern_add_recv(ghx_upattern* b, int32_t src_rank, int32_t src_id, int32_t dst_id,
+                          int32_t tag, const int64_t* gids, int64_t n_gids);
+int ghx_upattern_finish(ghx_upattern* b, ghx_pattern** out);
+int ghx_upattern_destroy(ghx_upattern* b);
 
 int ghx_pattern_destroy(ghx_pattern* p);
 /* A copy of a pattern whose send and receive halo maps keep only the keys whose remote rank is

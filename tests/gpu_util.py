@@ -42,6 +42,24 @@ class FakeContext:
         return r
 
 
+def unstructured_patterns(per_rank_domains, halo_gids=None):
+    """Every emulated rank's unstructured DomainDescriptors and its make_pattern<unstructured>:
+    per_rank_domains[r] = [(id, gids, outer_lids)], halo_gids[r] = that rank's halo generator
+    list (None: all outer gids). The ranks run as threads of this process (LoopbackWorld), each
+    passing only its own domains, as the reference's make_pattern does over MPI. Returns
+    [(dds, pattern_container)] in rank order."""
+    from ghex_amd import unstructured as U
+    from ghex_amd.context import LoopbackWorld
+
+    def rank_fn(ctx):
+        r = ctx.rank()
+        dds = [U.DomainDescriptor(i, g, o) for i, g, o in per_rank_domains[r]]
+        hg = U.HaloGenerator(None if halo_gids is None else halo_gids[r])
+        return dds, U.make_pattern(ctx, hg, dds)
+
+    return LoopbackWorld(len(per_rank_domains)).run(rank_fn)
+
+
 def emulated_exchange(cos, bis_per_rank, mixed=False):
     """Pack on every emulated rank, route send buffers to the matching recv buffers by
     (sender rank, domain pair, tag), unpack on every rank (all on one stream). mixed=True: the

@@ -343,7 +343,7 @@ def unstructured_direct(rank, world, cells, levels, reps):
     gids = gids[perm]
     outer = np.nonzero(perm >= cells)[0]
     ctx = ghex_amd.make_context()
-    dd = U.DomainDescriptor(rank, gids.tolist(), outer.tolist())
+    dd = U.DomainDescriptor(rank, gids, outer)
     pc = U.make_pattern(ctx, U.HaloGenerator(), [dd])
     want = gids.astype(np.float64)[:, None] * 100.0 + np.arange(levels)[None, :]
     init = want.copy()

@@ -231,3 +231,60 @@ def test_bulk_only_mode_reports_failed_children():
     assert len(lines) == 1
     o = json.loads(lines[0])
     assert o["mode"] == "bulk-only" and o["n_procs"] == 2 and "error" in o
+
+
+def test_config5_patterns_small_and_cpu_baseline_keys():
+    """config5_patterns (8 ranks' product make_pattern as threads) at a small size: every peer's
+    send list to rank 0 carries rank 0's receive gids; cpu_baseline_config5's keys, and its
+    bit-exact check against (here: numpy-computed) GPU buffers, including a detected mismatch."""
+    import numpy as np
+    import bench
+    pats, t_all, t_rank = bench.config5_patterns(world=8, cells=4000)
+    gids, outer, sends, recvs = pats[0]
+    assert len(sends) == 7 and len(recvs) == 7 and sum(len(l) for *_, l in recvs) == 200
+    for rid, rr, tag, lids in recvs:
+        pg, _, psend, _ = pats[rr]
+        plids = next(l for (i, q, tg, l) in psend if q == 0 and tg == tag)
+        assert np.array_equal(pg[plids], gids[lids])
+    levels = 8
+    host = gids.astype(np.float64)[:, None] * 100.0 + np.arange(levels)[None, :]
+    peer = [np.ascontiguousarray(host[l]).view(np.uint8).reshape(-1) for *_, l in recvs]
+    gpu = [np.ascontiguousarray(host[l]).view(np.uint8).reshape(-1) for *_, l in sends]
+    r = bench.cpu_baseline_config5(0.05, host, sends, recvs, peer, gpu, levels)
+    for k in ("value", "unit", "cores", "kind", "sample", "matches_gpu", "median_of_25_GBps"):
+        assert k in r, k
+    assert r["matches_gpu"] is True and r["cores"] == 1 and r["kind"] == "port"
+    gpu[3] = gpu[3].copy()
+    gpu[3][5] ^= 1
+    assert bench.cpu_baseline_config5(0.01, host, sends, recvs, peer, gpu, levels)["matches_gpu"] \
+        is False
+
+
+def test_cpu_baseline_config4_keys_and_parity_check():
+    """cpu_baseline_config4 on the full config-4 exchange: keys, and its field-byte comparison
+    with a packed message (here the oracle's own: equal; one flipped byte: detected)."""
+    import numpy as np
+    import bench
+    from oracle import oracle as orc
+    N, H = 256, 3
+    E = N + 2 * H
+    dom = orc.RegularDomain(0, (0, 0, 0), (N - 1,) * 3)
+    pat = orc.regular_make_pattern([[dom]], (0, 0, 0), (N - 1,) * 3, (H,) * 6, (1, 1, 1))[0][0]
+    val = np.arange(N ** 3, dtype=np.float64).reshape(N, N, N)
+    specs = []
+    for k, t in enumerate(bench.CONFIG4_TYPES):
+        dt = np.float64 if t == "f64" else np.float32
+        a = np.full((E, E, E), -1, dtype=dt)
+        a[H:H + N, H:H + N, H:H + N] = ((val + k) % (1 << 23)).astype(dt)
+        specs.append(orc.FieldSpec(a, a.itemsize, (2, 1, 0), (H,) * 3, (E,) * 3))
+    items = [(k, 0, pat, sp.elem, sp.elem, 1, 0) for k, sp in enumerate(specs)]
+    (sb,) = orc.plan_buffers(items, receive=False).values()
+    buf = np.zeros(sb.size, np.uint8)
+    for pf in sb.fields:
+        orc.structured_pack(specs[pf.field_index], buf, pf.boxes, pf.offset)
+    r = bench.cpu_baseline_config4(0.05, buf)
+    for k in ("value", "unit", "cores", "kind", "sample", "matches_gpu", "median_of_25_GBps"):
+        assert k in r, k
+    assert r["matches_gpu"] is True and r["value"] > 0
+    buf[sb.fields[2].offset + 11] ^= 1
+    assert bench.cpu_baseline_config4(0.01, buf)["matches_gpu"] is False

@@ -166,3 +166,51 @@ def test_unstructured_known_answer_gloo(golden_dir):
     with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
         case = json.load(fh)
     _run(4, _unstructured_worker, case)
+
+
+def _config5_worker(rank, world, cells):
+    """BASELINE config 5's domains (gids rank*10^7 + i, 5 % halo from the other
+    ranks, mt19937_64 seed 20260715, permuted storage) through the product's make_pattern over
+    gloo; then every halo value moved with the pattern's lid lists and checked."""
+    import time
+
+    import ghex_amd
+    from ghex_amd.communication_object import route
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
+    from tools import config5 as C5
+    gids, outer = C5.generate(rank, world, cells)
+    ctx = ghex_amd.make_context()
+    dist.barrier()
+    t0 = time.perf_counter()
+    dd = DomainDescriptor(rank, gids, outer)
+    pc = make_pattern(ctx, HaloGenerator(), [dd])
+    t_setup = time.perf_counter() - t0
+    # peak RSS of this process image (VmHWM: getrusage's ru_maxrss would also count the
+    # pytest parent's pages this spawned child held before its exec)
+    rss_gb = next(int(l.split()[1]) for l in open("/proc/self/status")
+                  if l.startswith("VmHWM:")) / 2 ** 20
+    f = gids.astype(np.float64) * 100.0
+    f[outer] = -1.0
+    st = [(rr, tag, torch.from_numpy(f[lids])) for rid, rr, tag, lids in pc.lid_arrays(0, 0)]
+    rt = [(rr, tag, torch.empty(len(lids), dtype=torch.float64), lids)
+          for rid, rr, tag, lids in pc.lid_arrays(0, 1)]
+    assert sum(len(x[3]) for x in rt) == len(outer)  # every outer cell is received once
+    for w in route(ctx, st, [(r, t, b) for r, t, b, _ in rt]):
+        w.wait()
+    for _, _, b, lids in rt:
+        f[lids] = b.numpy()
+    assert np.array_equal(f, gids.astype(np.float64) * 100.0)
+    print(f"rank {rank}: make_pattern {t_setup:.2f} s, peak RSS {rss_gb:.2f} GB", flush=True)
+    assert t_setup < 20.0, t_setup
+    assert rss_gb < 2.0, rss_gb
+
+
+def test_config5_pattern_full_size_gloo_two_ranks():
+    """make_pattern<unstructured> at BASELINE config 5's size per rank (10M cells, 500k halo
+    cells) over 2 gloo ranks: under 20 s and 2 GB peak RSS per rank (only reduced halos travel),
+    and the exchanged halo values are exact."""
+    _run(2, _config5_worker, 10_000_000)
+
+
+def test_config5_pattern_four_ranks_gloo():
+    _run(4, _config5_worker, 200_000)

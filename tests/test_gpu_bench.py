@@ -52,6 +52,16 @@ def test_bench_line_n1_small():
         assert x["verified"] is True and x["verified_fused"] is True, h
     c = r["cold_clean_kernel_events_us"]
     assert c["pack"] > 0 and c["unpack"] > 0 and c["step_pack"] > 0 and c["step_unpack"] > 0
+    # the other BASELINE configs: each verifies the launches it times
+    ex = d["extra_configs"]
+    c4 = ex["config4_5fields_256^3_h3_f64f32"]
+    assert c4["verified"] is True and c4["verified_fused"] is True and "timed hipGraph" in \
+        c4["verified_what"]
+    for lv in (1, 8):
+        c5 = ex[f"config5_unstructured_10M_5pct_levels{lv}"]
+        assert c5["verified"] is True and c5["halo_cells"] == 500_000 and c5["peers"] == 7, c5
+        assert "cpu_baseline" not in c5  # --no-cpu-baseline
+    assert ex["config5_pattern_setup"]["ranks"] == 8
 
 
 def test_bench_spawns_two_ranks_rehearsal():
@@ -63,7 +73,9 @@ def test_bench_spawns_two_ranks_rehearsal():
         assert x["verified"] is True, h
     assert d["config"]["decomposition"] == [2, 1, 1] and d["config"]["world_size"] == 2
     assert d["exchange_pipelined"]["verified"] is True
-    assert d["unstructured_exchange"].get("verified") is True, d["unstructured_exchange"]
+    u = d["unstructured_exchange"]
+    assert u.get("verified") is True and u["cells_per_rank"] == 10_000_000, u
+    assert u["halo_cells_per_rank"] == 500_000 and u["setup_s"] < 60, u
     assert "extras_error" not in d, d.get("extras_error")
 
 

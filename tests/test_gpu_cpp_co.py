@@ -63,6 +63,51 @@ def test_co_loopback_all_gather_cpu(tmp_path):
     assert subprocess.run([str(exe)], timeout=60).returncode == 0
 
 
+def test_co_unstructured_make_pattern_known_answer_cpu(tmp_path, golden_dir):
+    """The C++ make_pattern<unstructured> (reduced halos through the transport's all_gather) on
+    4 loopback threads, no GPU: every rank's send/recv lid tables equal the reference's
+    known-answer tables (unstructured_test_case.hpp:217-343)."""
+    import json
+    with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
+        case = json.load(fh)
+    doms, exp = [], []
+    for r in range(4):
+        d = case["domains"][str(r)]
+        doms.append("{%s}, {%s}" % (",".join(map(str, d["gids"])), ",".join(map(str, d["halo_lids"]))))
+        for direction, key in ((0, "send_maps"), (1, "recv_maps")):
+            for rid, lids in sorted(case[key][str(r)].items(), key=lambda kv: int(kv[0])):
+                exp.append("{%d,%d,%s,{%s}}" % (r, direction, rid, ",".join(map(str, lids))))
+    src = tmp_path / "u.cpp"
+    src.write_text(
+        '#include <ghex_amd/communication_object.hpp>\n#include <thread>\n#include <map>\n'
+        'namespace U = ghex_amd::unstructured;\n'
+        'struct E { int r, dir, rid; std::vector<long> lids; };\n'
+        'int main(){ std::vector<std::pair<std::vector<long>, std::vector<long>>> doms = {'
+        + ",".join("{%s}" % d for d in doms) + '};\n'
+        '  std::vector<E> exp = {' + ",".join(exp) + '};\n'
+        '  ghex_amd::loopback_hub hub(4); int bad = 0; std::mutex m;\n'
+        '  std::vector<std::thread> th; for (int r = 0; r < 4; ++r) th.emplace_back([&, r]{\n'
+        '    ghex_amd::loopback_transport t(hub, r); ghex_amd::context ctx(t);\n'
+        '    U::domain_descriptor d(r, doms[r].first, doms[r].second);\n'
+        '    auto pc = U::make_pattern(ctx, {}, {d});\n'
+        '    std::map<std::pair<int,int>, std::vector<long>> got;\n'
+        '    for (int dir = 0; dir < 2; ++dir) { int32_t nk = 0; ghx_pattern_num_keys(pc.handle(), 0, dir, &nk);\n'
+        '      for (int k = 0; k < nk; ++k) { int32_t rid, rr, tag, ns; int64_t ne;\n'
+        '        ghx_pattern_key(pc.handle(), 0, dir, k, &rid, &rr, &tag, &ns, &ne);\n'
+        '        std::vector<long> l(ne); ghx_pattern_key_lids(pc.handle(), 0, dir, k, l.data(), ne);\n'
+        '        got[{dir, rid}] = l; } }\n'
+        '    std::lock_guard<std::mutex> g(m); std::size_t n = 0;\n'
+        '    for (auto& e : exp) if (e.r == r) { ++n; if (got[{e.dir, e.rid}] != e.lids) ++bad; }\n'
+        '    if (n != got.size()) ++bad; });\n'
+        '  for (auto& t : th) t.join(); return bad ? 1 : 0; }\n')
+    exe = tmp_path / "u"
+    subprocess.run(["g++", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__", "-I", INC, "-I",
+                    "/opt/rocm/include", str(src), "-o", str(exe), "-L", LIB, "-lghx",
+                    "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{LIB}",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    assert subprocess.run([str(exe)], timeout=60).returncode == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("parts,N,H", [((1, 1, 1), 12, 2), ((2, 1, 1), 10, 2),
                                        ((2, 2, 1), 9, 1), ((2, 2, 2), 8, 3),

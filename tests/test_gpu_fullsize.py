@@ -145,18 +145,18 @@ def test_unstructured_known_answer_on_device(golden_dir):
     import os
     import torch
     from ghex_amd import unstructured as U
-    from tests.gpu_util import FakeContext
+    from tests.gpu_util import FakeContext, unstructured_patterns
     with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
         case = json.load(fh)
     L = 3
-    table = {r: [(r, case["domains"][str(r)]["gids"], case["domains"][str(r)]["halo_lids"], None)]
-             for r in range(4)}
+    table = {r: [] for r in range(4)}
+    pats = unstructured_patterns([[(r, case["domains"][str(r)]["gids"],
+                                    case["domains"][str(r)]["halo_lids"])] for r in range(4)])
     for levels_first in (True, False):
         pcs, fields, cos, bis = [], [], [], []
         for r in range(4):
             d = case["domains"][str(r)]
-            dd = U.DomainDescriptor(r, d["gids"], d["halo_lids"])
-            pc = U.make_pattern(FakeContext(r, 4, table), U.HaloGenerator(), [dd])
+            (dd,), pc = pats[r]
             n = len(d["gids"])
             host = np.full((n, L), -1.0)
             for lid, gid in enumerate(d["gids"]):

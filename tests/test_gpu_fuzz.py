@@ -276,17 +276,17 @@ def _ufield(torch, n, f, rng):
 def _setup_unstructured(case):
     import torch
     from ghex_amd import unstructured as U
-    from tests.gpu_util import FakeContext
+    from tests.gpu_util import FakeContext, unstructured_patterns
     nr = case["nr"]
-    table = {r: [(d["id"], d["gids"], d["outer"], None) for d in case["doms"] if d["rank"] == r]
-             for r in range(nr)}
+    table = {r: [] for r in range(nr)}
     rng = np.random.default_rng(case["seed"] + 7)
     cos, bis_all, recs = [], [], []
+    pats = unstructured_patterns([[(d["id"], d["gids"], d["outer"]) for d in case["doms"]
+                                   if d["rank"] == r] for r in range(nr)])
     for r in range(nr):
         ctx = FakeContext(r, nr, table)
         mine = [d for d in case["doms"] if d["rank"] == r]
-        dds = [U.DomainDescriptor(d["id"], d["gids"], d["outer"]) for d in mine]
-        pc = U.make_pattern(ctx, U.HaloGenerator(), dds)
+        dds, pc = pats[r]
         bis = []
         for f in case["fields"]:
             for dd, d in zip(dds, mine):

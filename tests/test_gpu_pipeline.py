@@ -104,15 +104,14 @@ def test_per_buffer_plans_unstructured(golden_dir):
     import os
     import torch
     from ghex_amd import unstructured as U
-    from tests.gpu_util import FakeContext
+    from tests.gpu_util import FakeContext, unstructured_patterns
     with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
         case = json.load(fh)
-    table = {r: [(r, case["domains"][str(r)]["gids"], case["domains"][str(r)]["halo_lids"], None)]
-             for r in range(4)}
-    for r in range(4):
+    table = {r: [] for r in range(4)}
+    doms = [[(r, case["domains"][str(r)]["gids"], case["domains"][str(r)]["halo_lids"])]
+            for r in range(4)]
+    for r, ((dd,), pc) in enumerate(unstructured_patterns(doms)):
         d = case["domains"][str(r)]
-        dd = U.DomainDescriptor(r, d["gids"], d["halo_lids"])
-        pc = U.make_pattern(FakeContext(r, 4, table), U.HaloGenerator(), [dd])
         t = torch.arange(len(d["gids"]) * 3, dtype=torch.float64).view(-1, 3).cuda()
         co = U.make_communication_object(FakeContext(r, 4, table))
         _per_buffer_vs_fused(co, [pc(U.make_field_descriptor(dd, t))])

@@ -112,27 +112,19 @@ def test_regular_pattern_cubes(parts, halos, periodic):
         _cmp_regular(pc, opat[r], 3)
 
 
-def _unstructured_abi(doms_ranks, halo_gids, my_rank):
+def _unstructured_abi(doms_ranks, halo_gids):
+    """Every rank's make_pattern<unstructured>, run as threads of this process (LoopbackWorld):
+    each rank passes only its own domains; returns the pattern containers in rank order."""
+    from ghex_amd.context import LoopbackWorld
     from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
 
-    class FakeCtx:
-        def rank(self):
-            return my_rank
+    def rank_fn(ctx):
+        r = ctx.rank()
+        mine = [DomainDescriptor(d.id, d.gids, d.outer_lids) for d in doms_ranks[r]]
+        hg = HaloGenerator(None if halo_gids is None else halo_gids[r][0])
+        return make_pattern(ctx, hg, mine)
 
-        def size(self):
-            return len(doms_ranks)
-
-        def all_gather_object(self, obj):
-            out = []
-            for r, doms in enumerate(doms_ranks):
-                out.append([(d.id, d.gids, d.outer_lids,
-                             None if halo_gids is None else halo_gids[r][i])
-                            for i, d in enumerate(doms)])
-            return out
-
-    mine = [DomainDescriptor(d.id, d.gids, d.outer_lids) for d in doms_ranks[my_rank]]
-    hg = HaloGenerator(None if halo_gids is None else halo_gids[my_rank][0])
-    return make_pattern(FakeCtx(), hg, mine)
+    return LoopbackWorld(len(doms_ranks)).run(rank_fn)
 
 
 class _UD:
@@ -144,8 +136,7 @@ def test_unstructured_pattern_known_answer(golden_dir):
     with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
         case = json.load(fh)
     doms = [[_UD(int(k), v["gids"], v["halo_lids"])] for k, v in sorted(case["domains"].items())]
-    for r in range(4):
-        pc = _unstructured_abi(doms, None, r)
+    for r, pc in enumerate(_unstructured_abi(doms, None)):
         sends = {str(rid): lids for rid, rr, tag, lids in pc.send_halos(0)}
         recvs = {str(rid): lids for rid, rr, tag, lids in pc.recv_halos(0)}
         assert sends == case["send_maps"][str(r)]
@@ -160,8 +151,7 @@ def test_unstructured_pattern_matches_oracle_with_repeats(golden_dir):
     hg = [[v["outer"]] for k, v in items]
     odoms = [[orc.UnstructuredDomain(int(k), v["all"], v["outer_lids"])] for k, v in items]
     opats = orc.unstructured_make_pattern(odoms, hg)
-    for r in range(4):
-        pc = _unstructured_abi(doms, hg, r)
+    for r, pc in enumerate(_unstructured_abi(doms, hg)):
         for direction, key in ((0, "send"), (1, "recv")):
             got = [(rr, tag, rid, lids) for rid, rr, tag, lids in pc.halos(0, direction)]
             exp = [(rr, tag, rid, lids) for (rr, tag), (rid, lids) in opats[r][0][key].items()]
@@ -349,3 +339,39 @@ def test_pattern_filter_splits_local_and_remote_halos():
             assert ka == [h for h in whole if h[1] in sel]
             assert kb == [h for h in whole if h[1] not in sel]
             assert sorted(ka + kb) == sorted(whole)
+
+
+@pytest.mark.parametrize("world,cells,halo", [(2, 3000, 150), (3, 2000, 100), (8, 500, 25)])
+def test_unstructured_pattern_config5_domains_match_oracle(world, cells, halo):
+    """The reduced-halo make_pattern (every rank passes only its own domain; LoopbackWorld
+    threads) against the oracle's all-ranks restatement of unstructured/pattern.hpp:187-370, on
+    BASELINE config 5's domain generation (tools/config5_gen.cpp) at small sizes."""
+    from tools import config5 as C5
+    doms = [C5.generate(r, world, cells, halo) for r in range(world)]
+    odoms = [[orc.UnstructuredDomain(r, g.tolist(), o.tolist())] for r, (g, o) in enumerate(doms)]
+    opats = orc.unstructured_make_pattern(odoms)
+    pcs = _unstructured_abi([[_UD(r, g, o)] for r, (g, o) in enumerate(doms)], None)
+    for r, pc in enumerate(pcs):
+        for direction, key in ((0, "send"), (1, "recv")):
+            got = [(rr, tag, rid, list(lids)) for rid, rr, tag, lids in pc.halos(0, direction)]
+            exp = [(rr, tag, rid, lids) for (rr, tag), (rid, lids) in opats[r][0][key].items()]
+            assert got == exp
+        assert sum(len(l) for *_, l in pc.recv_halos(0)) == halo
+
+
+def test_unstructured_domain_errors_match_reference():
+    """domain_descriptor's constructor and make_outer_lids errors (user_concepts.hpp:88-175)."""
+    from ghex_amd import _ghx
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator
+    with pytest.raises(_ghx.GhxError, match="repeated outer"):
+        DomainDescriptor(0, [1, 2, 3], [1, 1])
+    with pytest.raises(_ghx.GhxError, match="repeated inner"):
+        DomainDescriptor(0, [1, 2, 1], [1])
+    d = DomainDescriptor(0, [5, 7, 7, 9], [1, 2])  # gid 7 held by two outer cells
+    assert d.inner_size() == 2 and d.size() == 4
+    assert list(d.halo_gids(HaloGenerator())) == [7, 7]
+    assert list(d.halo_gids(HaloGenerator([9, 7, 7]))) == [7, 7]  # 9 is inner: skipped
+    with pytest.raises(_ghx.GhxError, match="not often enough"):
+        d.halo_gids(HaloGenerator([7]))
+    with pytest.raises(_ghx.GhxError, match="associated lid"):
+        d.halo_gids(HaloGenerator([7, 7, 7]))
