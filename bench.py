@@ -231,14 +231,17 @@ class Runner:
 def verify_replay(torch, dev, replay, clear, count_bad, send, recv, deliver=None):
     """Wrong cells after the TIMED kernels alone: halos reset (clear), every send/recv buffer
     byte set to 0xFF (an fp64 NaN, unequal to every expected value), the timed graph replayed
-    (replay), then — where peer messages exist — deliver() moves the packed send buffers to the
-    receivers and unpacks them; count_bad() checks every cell (summed over ranks)."""
+    (replay: the same graph replays the timed region ran). Where peer messages exist, deliver()
+    then moves the packed send buffers into the receivers' receive buffers (transport only) and
+    the timed graph is replayed once more, so the peer halos too are written by the timed
+    graph's own unpack launch. count_bad() checks every cell (summed over ranks)."""
     clear()
     for t in list(send) + list(recv):
         t.fill_(255)
     replay()
     if deliver is not None:
         deliver()
+        replay()
     torch.cuda.synchronize(dev)
     return count_bad()
 
@@ -620,19 +623,18 @@ def main():
     t_recvs = [(x["rank"], x["tag"], recv[i][:x["size"]]) for i, x in enumerate(plan.recv)
                if x["rank"] != me]
 
-    def transport_unpack():
-        """Deliver the send buffers the replay packed, then unpack them (N>1)."""
+    def transport():
+        """Deliver the send buffers the replay packed into the receive buffers (N>1)."""
         from ghex_amd.communication_object import route
         if args.rehearse:
             co._exchange_host_staged(plan, t_sends, t_recvs, stream)
         else:
             for w in route(ctx, t_sends, t_recvs):
                 w.wait()
-        unpack(stream.cuda_stream)
 
     with guard.stage("verify_timed", args.exchange_timeout):
         verified = verify_replay(torch, dev, lambda: runner.run(K), clear_halos, verify,
-                                 send, recv, transport_unpack if t_recvs else None) == 0
+                                 send, recv, transport if t_recvs else None) == 0
     value = world * step_bytes * K / T / 1e9
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
@@ -651,9 +653,12 @@ def main():
             "world_size": world, "backend": backend,
         },
         "verified": verified,
-        "verified_what": "the timed hipGraph (k_copy pack + k_copy unpack) replayed once after "
-                         "the timed region on halos reset to -1 and buffers set to 0xFF" +
-                         ("" if world == 1 else ", then transport + unpack") +
+        "verified_what": "after the timed region, on halos reset to -1 and every buffer byte "
+                         "set to 0xFF: the timed hipGraphs (k_copy pack + k_copy unpack, K "
+                         "steps) replayed" +
+                         ("" if world == 1 else ", the peer messages transported into the "
+                                                "receive buffers, the timed hipGraphs replayed "
+                                                "again (the peer halos written by their unpack)") +
                          "; every cell of every rank checked",
         "verified_fused": verified_fused,
         "verified_fused_what": ("the first exchange: co.exchange() = the fused k_self launch"
@@ -1399,7 +1404,6 @@ def bench_halo(h, v, torch, dist, dev, stream, args, x_alloc=None):
         else:
             for wk in route(v["ctx"], t_sends, t_recvs):
                 wk.wait()
-        unpack(stream.cuda_stream)
     # `verified`: the timed graph itself (k_copy pack + unpack), replayed on reset halos/buffers
     bad = verify_replay(torch, dev, lambda: runner.run(K), clear, count_bad, send, recv,
                         deliver if t_recvs else None)

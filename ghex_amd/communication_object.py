@@ -780,9 +780,22 @@ class CommunicationObject:
         self._direct = {}
 
     # low-level access for benchmarks / tests (no transport)
+    def _plain_plan(self, bis):
+        """The plan of `bis` for the single-buffered low-level helpers below. A direct object's
+        plan, once its first exchange has set the epoch parity (ghx_exchange_set_parity), packs
+        into and unpacks from the copy of the exchange's parity: with this object's single-size
+        local send buffers that would write past their end, so it is refused."""
+        plan = self.plan(bis)
+        d = self.__dict__.get("_direct", {}).get(id(plan))
+        if d is not None and d.get("ep") is not None:
+            raise RuntimeError("pack_only / unpack_only and their mixed forms are not available "
+                               "on a direct exchange's plan (its launches are double-buffered "
+                               "by epoch parity); use exchange()")
+        return plan
+
     def pack_only(self, bis, stream=None):
         import torch
-        plan = self.plan(bis)
+        plan = self._plain_plan(bis)
         send, recv = self.buffers(plan, bis[0].field.device)
         s = (stream or torch.cuda.current_stream()).cuda_stream
         _ghx.call("ghx_exchange_pack", plan.h, _ghx.ptr_array([b.field.data_ptr() for b in bis]),
@@ -792,7 +805,7 @@ class CommunicationObject:
     def pack_self_only(self, bis, stream=None):
         """Mixed exchanges: pack every send buffer and complete the self messages."""
         import torch
-        plan = self.plan(bis)
+        plan = self._plain_plan(bis)
         send, recv = self.buffers(plan, bis[0].field.device)
         s = (stream or torch.cuda.current_stream()).cuda_stream
         _ghx.call("ghx_exchange_pack_self", plan.h,
@@ -803,7 +816,7 @@ class CommunicationObject:
     def unpack_peers_only(self, bis, stream=None):
         """Mixed exchanges: unpack the peer messages only."""
         import torch
-        plan = self.plan(bis)
+        plan = self._plain_plan(bis)
         send, recv = self.buffers(plan, bis[0].field.device)
         s = (stream or torch.cuda.current_stream()).cuda_stream
         _ghx.call("ghx_exchange_unpack_peers", plan.h,
@@ -813,7 +826,7 @@ class CommunicationObject:
 
     def unpack_only(self, bis, stream=None):
         import torch
-        plan = self.plan(bis)
+        plan = self._plain_plan(bis)
         send, recv = self.buffers(plan, bis[0].field.device)
         s = (stream or torch.cuda.current_stream()).cuda_stream
         _ghx.call("ghx_exchange_unpack", plan.h,

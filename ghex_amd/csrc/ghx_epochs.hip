@@ -124,7 +124,10 @@ __device__ __forceinline__ void dev_store(uint64_t* p, uint64_t v)
 
 __device__ __forceinline__ unsigned xcc_id()
 {
-    // HW_REG_XCC_ID (hwreg 20), bits 3:0: the XCD this wave runs on (gfx940+)
+    // HW_REG_XCC_ID (hwreg 20), bits 3:0: the XCD this wave runs on (gfx940+). The close kernels
+    // use it modulo the partition's XCD count (hipDeviceAttributeNumberOfXccs): in a partitioned
+    // mode (DPX/CPX) the register may report the physical XCD (e.g. 4..7 of a 4-XCD partition),
+    // whose residues are still one slot per XCD. Only the unpartitioned (SPX) mode has run here.
     return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf;
 }
 
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(64) void k_epoch_close(epoch_args a)
     const uint64_t e = dev_load(at(dv, 0));
     const bool open_failed = dev_load(at(dv, 0) + 1) == e;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (a.n_tgt > 0 && lane == 0) dev_store(at(dv, d_rel(int(xcc_id()))), e);
+    if (a.n_tgt > 0 && lane == 0) dev_store(at(dv, d_rel(int(xcc_id() % unsigned(a.n_xcc)))), e);
     if (blockIdx.x == 0)
     {
         uint64_t seen = 0;
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(64) void k_epoch_close1(epoch_args a)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
     {
-        if (a.n_tgt > 0) dev_store(at(dv, d_rel(int(xcc_id()))), e);
+        if (a.n_tgt > 0) dev_store(at(dv, d_rel(int(xcc_id() % unsigned(a.n_xcc)))), e);
         __hip_atomic_fetch_add(at(dv, d_arrive), uint64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (blockIdx.x == 0)
@@ -319,14 +322,20 @@ struct ghx_epochs
     bool registered = false;
     uint64_t* dev = nullptr;
     uint64_t* box = nullptr;                 // this rank's inbox (fine-grained device memory)
-    std::vector<std::pair<int, void*>> imports;  // (node-local rank, IPC mapping of its inbox)
+    struct import_t
+    {
+        int rank;        // node-local rank
+        void* base;      // its inbox allocation's IPC mapping (what hipIpcCloseMemHandle takes)
+        uint64_t* box;   // its inbox inside that mapping
+    };
+    std::vector<import_t> imports;
     int fence_groups = 0;
     int mode = -1;  // 0: open + close (phases 0, 1); 1: one-launch close (phase 2)
     epoch_args args{};
     void close_imports()
     {
-        for (auto& kv : imports)
-            if (kv.second) (void)hipIpcCloseMemHandle(kv.second);
+        for (auto& im : imports)
+            if (im.base) (void)hipIpcCloseMemHandle(im.base);
         imports.clear();
     }
     ~ghx_epochs()
@@ -341,8 +350,8 @@ struct ghx_epochs
     // process, e.g. two ranks as threads of one process)
     uint64_t* inbox_of(int r)
     {
-        for (auto& kv : imports)
-            if (kv.first == r) return static_cast<uint64_t*>(kv.second);
+        for (auto& im : imports)
+            if (im.rank == r) return im.box;
         const volatile uint64_t* meta = line(l_handle(r) + 1);
         if (meta[3] != kMagic) throw invalid("a peer has not published its epoch inbox (not attached?)");
         if (int64_t(meta[1]) == int64_t(getpid())) return reinterpret_cast<uint64_t*>(meta[2]);
@@ -351,8 +360,9 @@ struct ghx_epochs
         void* p = nullptr;
         if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
             throw hip_error("hipIpcOpenMemHandle(a peer's epoch inbox)");
-        imports.emplace_back(r, p);
-        return static_cast<uint64_t*>(p) + meta[0] / sizeof(uint64_t);
+        uint64_t* b = static_cast<uint64_t*>(p) + meta[0] / sizeof(uint64_t);
+        imports.push_back({r, p, b});
+        return b;
     }
     volatile uint64_t* line(size_t l) const { return static_cast<volatile uint64_t*>(host) + l * 8; }
 };
@@ -481,6 +491,10 @@ int ghx_epochs_peers(ghx_epochs* ep, const int32_t* sources, int32_t n_sources,
             if (r < 0 || r >= ep->args.world || r == ep->args.rank)
                 throw invalid("peer out of range of the node-local group (or this rank itself)");
         }
+        // kernels already enqueued or captured hold the peers' inbox pointers by value: the
+        // mappings must not change under them
+        if (ep->mode >= 0)
+            throw invalid("ghx_epochs_peers: peers are fixed once the epochs have been enqueued");
         // the peers' inboxes (every peer has attached: the caller's setup passed its barrier)
         ep->close_imports();
         ep->args.n_src = ep->args.n_tgt = 0;

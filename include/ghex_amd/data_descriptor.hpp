@@ -14,15 +14,26 @@
 // neighbour, unstructured/pattern.hpp:324-325). Each list becomes one fused libghx launch with
 // the indices resident in device memory (the reference reads them from managed memory).
 //
+// Plans: the first pack/unpack of an index list uploads it once (ghx_uplan_create); later calls
+// with the same list find the plan by the list's address, length and index width, O(1) host
+// work per call. This relies on the reference's contract that the pattern's index containers are
+// immutable and outlive every exchange that uses them (include/ghex/pattern_container.hpp:84-87);
+// call forget_plans() after changing a list in place. (The plain C entry points
+// ghx_unstructured_pack/unpack compare the whole list on every call instead.)
+//
 // Depends only on <ghx.h> and the standard library; link with -lghx.
 #pragma once
 
 #include <ghx.h>
 
 #include <cstdint>
+#include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <type_traits>
+#include <vector>
 
 namespace ghex_amd
 {
@@ -52,6 +63,10 @@ class data_descriptor
     value_type* m_values;
     device_id_type m_device_id;
     ghx_udata_desc m_desc{};
+    // (list address, length, index bytes, direction) -> plan; shared by copies of the descriptor
+    using plan_key = std::tuple<const void*, std::size_t, int32_t, int32_t>;
+    using plan_map = std::map<plan_key, std::shared_ptr<ghx_uplan>>;
+    std::shared_ptr<plan_map> m_plans = std::make_shared<plan_map>();
 
   public:
     /** values: device pointer to domain_size * levels elements (plus padding when
@@ -97,28 +112,46 @@ class data_descriptor
     template<typename IndexContainer>
     void pack(value_type* buffer, const IndexContainer& c, void* stream_ptr)
     {
-        for (const auto& is : c)
-        {
-            const auto& l = is.local_indices();
-            check_u(ghx_unstructured_pack(&m_desc, m_values, buffer, l.data(), lid_bytes(l),
-                                          int64_t(l.size()), stream_of(stream_ptr)),
-                    "ghx_unstructured_pack");
-        }
+        for (const auto& is : c) run(is.local_indices(), 0, buffer, stream_ptr);
     }
 
     template<typename IndexContainer>
     void unpack(const value_type* buffer, const IndexContainer& c, void* stream_ptr)
     {
         for (const auto& is : c)
-        {
-            const auto& l = is.local_indices();
-            check_u(ghx_unstructured_unpack(&m_desc, m_values, buffer, l.data(), lid_bytes(l),
-                                            int64_t(l.size()), stream_of(stream_ptr)),
-                    "ghx_unstructured_unpack");
-        }
+            run(is.local_indices(), 1, const_cast<value_type*>(buffer), stream_ptr);
     }
 
+    // drop the cached plans (after an index list was changed in place)
+    void forget_plans() { m_plans->clear(); }
+
   private:
+    template<typename V>
+    void run(const V& l, int32_t dir, value_type* buffer, void* stream_ptr)
+    {
+        if (l.empty()) return;
+        const plan_key key{static_cast<const void*>(l.data()), l.size(), lid_bytes(l), dir};
+        auto it = m_plans->find(key);
+        if (it == m_plans->end())
+        {
+            std::vector<int64_t> wide(l.begin(), l.end());
+            ghx_upack_entry e{};
+            e.data = m_desc;
+            e.field_slot = 0;
+            e.buffer_slot = 0;
+            e.buffer_offset = 0;
+            e.lids = wide.data();
+            e.n_lids = int64_t(wide.size());
+            ghx_uplan* p = nullptr;
+            check_u(ghx_uplan_create(&e, 1, dir, &p), "ghx_uplan_create");
+            it = m_plans->emplace(key, std::shared_ptr<ghx_uplan>(p, ghx_uplan_destroy)).first;
+        }
+        void* f[1] = {m_values};
+        void* b[1] = {buffer};
+        check_u(ghx_uplan_execute(it->second.get(), f, 1, b, 1, stream_of(stream_ptr)),
+                dir ? "unpack: ghx_uplan_execute" : "pack: ghx_uplan_execute");
+    }
+
     template<typename V>
     static int32_t lid_bytes(const V&)
     {

@@ -482,7 +482,8 @@ int ghx_put_destroy(ghx_put* put);
  * epoch and error for the host (the creating rank passes create = 1 before the others attach
  * with 0, and one rank unlinks the name once all have attached). `world` and `rank` are the node-local group's size
  * and this rank's index in it (one block per host; at most 64 ranks per host). ghx_epochs_peers
- * sets this rank's sources (ranks that write into its memory) and targets (ranks whose memory it
+ * (before the first ghx_epochs_enqueue; refused afterwards: enqueued kernels hold the peers'
+ * inbox mappings) sets this rank's sources (ranks that write into its memory) and targets (ranks whose memory it
  * writes into) as node-local indices, excluding itself. Open: this rank's halos / receive
  * buffers are open to its sources; wait until each target has opened. Close: system-scope
  * release on every XCD (the grid is sized from the queried XCD count; the leader checks that

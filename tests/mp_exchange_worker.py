@@ -164,6 +164,17 @@ def main():
             if mode == "direct":
                 for _ in range(reps):
                     co.exchange([pc(fd)]).wait()
+                if world > 1:
+                    # the single-buffered helpers refuse a plan with epoch parity set (they would
+                    # pack past the end of the local send buffers)
+                    for helper in (co.pack_only, co.unpack_only, co.pack_self_only,
+                                   co.unpack_peers_only):
+                        try:
+                            helper([pc(fd)])
+                        except RuntimeError as e:
+                            assert "direct exchange" in str(e), e
+                        else:
+                            raise AssertionError(f"{helper.__name__} ran on a direct plan")
             elif mode == "directloop":
                 # back to back on the stream, one host wait at the end: the ranks' devices stay
                 # in step through the epochs alone (tools/prof_direct.sh traces this)
