@@ -68,7 +68,7 @@ def test_bench_spawns_two_ranks_rehearsal():
     d = _bench("--gpus", "2", "--rehearse", "--N", "64", "--steps", "10", "--warmup", "2",
                "--no-cold", timeout=240)
     assert d["n_gpus"] == 2 and d["verified"] is True and d["verified_fused"] is True
-    assert "transport + unpack" in d["verified_what"]
+    assert "transported into the receive buffers" in d["verified_what"]
     for h, x in d["halo_widths"].items():
         assert x["verified"] is True, h
     assert d["config"]["decomposition"] == [2, 1, 1] and d["config"]["world_size"] == 2
