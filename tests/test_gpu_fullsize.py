@@ -180,3 +180,51 @@ def test_unstructured_known_answer_on_device(golden_dir):
                 for lid in lids:
                     for l in range(L):
                         assert got[lid, l] == rid * 10000 + d["gids"][lid] * 100 + l
+
+
+@pytest.mark.parametrize("levels,levels_first", [(1, True), (8, True), (3, False)])
+def test_config5_product_pattern_full_size(levels, levels_first):
+    """BASELINE config 5 at its size through the PRODUCT pattern: 8 emulated ranks, each 10M
+    cells + 500k halo cells (tools/config5_gen.cpp), make_pattern<unstructured> run as 8 threads
+    (reduced halos), CommunicationObject plans, fused device pack of every rank, messages routed,
+    fused device unpack. Rank 0's packed send buffers equal the oracle's data_descriptor<cpu>::get
+    over the same lid lists, bit for bit; every cell of every rank holds its owner's value
+    (gid*100 + level) afterwards."""
+    import torch
+    from ghex_amd import unstructured as U
+    from tests.gpu_util import FakeContext, emulated_exchange, unstructured_patterns
+    from tools import config5 as C5
+    W = 8
+    doms = [C5.generate(r, W) for r in range(W)]
+    pats = unstructured_patterns([[(r, g, o)] for r, (g, o) in enumerate(doms)])
+    cos, bis, fields, hosts = [], [], [], []
+    for r, ((dd,), pc) in enumerate(pats):
+        g, o = doms[r]
+        host = g.astype(np.float64)[:, None] * 100.0 + np.arange(levels)[None, :]
+        init = host.copy()
+        init[o] = -1.0
+        t = torch.from_numpy(init).cuda()
+        if not levels_first:
+            t = t.t().contiguous().t()
+        fd = U.make_field_descriptor(dd, t)
+        assert fd.levels_first == levels_first
+        fields.append(t)
+        hosts.append(host)
+        cos.append(U.make_communication_object(FakeContext(r, W, {q: [] for q in range(W)})))
+        bis.append([pc(fd)])
+    plans, bufs = emulated_exchange(cos, bis)
+    # rank 0's send buffers vs the oracle's get (levels-first: index stride L; last: level
+    # stride n)
+    g0, o0 = doms[0]
+    n0 = g0.size
+    vals0 = np.ascontiguousarray(hosts[0] if levels_first else hosts[0].T).reshape(-1)
+    isd, lsd = (levels, 1) if levels_first else (1, n0)
+    sends = {(rr, tag): lids for rid, rr, tag, lids in pats[0][1].lid_arrays(0, 0)}
+    for i, x in enumerate(plans[0].send):
+        lids = sends[(x["rank"], x["tag"])]
+        ob = np.zeros(len(lids) * levels * 8, np.uint8)
+        orc.unstructured_get(vals0, ob, 8, lids, levels, levels_first, isd, lsd)
+        assert np.array_equal(bufs[0][0][i][:x["size"]].cpu().numpy(), ob), x
+    for r in range(W):
+        got = fields[r].cpu().numpy()
+        assert np.array_equal(got, hosts[r]), r
