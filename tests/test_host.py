@@ -375,3 +375,32 @@ def test_unstructured_domain_errors_match_reference():
         d.halo_gids(HaloGenerator([7]))
     with pytest.raises(_ghx.GhxError, match="associated lid"):
         d.halo_gids(HaloGenerator([7, 7, 7]))
+
+
+@pytest.mark.parametrize("grouping", [[[0, 1], [2, 3]], [[3], [0, 2], [1]], [[0, 1, 2, 3]]])
+def test_unstructured_pattern_multi_domain_ranks_match_oracle(golden_dir, grouping):
+    """Several domains per rank (the reference's tag layout shifts the source domain's local
+    index by num_bits(max domains per rank), unstructured/pattern.hpp:230-233; self messages
+    between two domains of one rank): the 4-domain known-answer case grouped onto 1-3 ranks,
+    product (LoopbackWorld ranks, own domains only) vs the oracle."""
+    with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
+        case = json.load(fh)
+    d = case["domains"]
+    doms = [[_UD(i, d[str(i)]["gids"], d[str(i)]["halo_lids"]) for i in g] for g in grouping]
+    odoms = [[orc.UnstructuredDomain(x.id, x.gids, x.outer_lids) for x in g] for g in doms]
+    opats = orc.unstructured_make_pattern(odoms)
+    from ghex_amd.context import LoopbackWorld
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
+
+    def rank_fn(ctx):
+        mine = [DomainDescriptor(x.id, x.gids, x.outer_lids) for x in doms[ctx.rank()]]
+        return make_pattern(ctx, HaloGenerator(), mine)
+
+    for r, pc in enumerate(LoopbackWorld(len(grouping)).run(rank_fn)):
+        assert len(pc) == len(grouping[r])
+        for li in range(len(pc)):
+            for direction, key in ((0, "send"), (1, "recv")):
+                got = [(rr, tag, rid, lids) for rid, rr, tag, lids in pc.halos(li, direction)]
+                exp = [(rr, tag, rid, lids)
+                       for (rr, tag), (rid, lids) in opats[r][li][key].items()]
+                assert got == exp, (r, li, key)
