@@ -404,3 +404,58 @@ def test_unstructured_pattern_multi_domain_ranks_match_oracle(golden_dir, groupi
                 exp = [(rr, tag, rid, lids)
                        for (rr, tag), (rid, lids) in opats[r][li][key].items()]
                 assert got == exp, (r, li, key)
+
+
+@pytest.mark.parametrize("block", range(8))
+def test_unstructured_pattern_random_meshes_match_oracle(block):
+    """200 seeded random meshes (tests/test_gpu_fuzz.py::draw_unstructured: 1-4 ranks with 1-2
+    domains each, repeated halo gids, random storage orders), half with an explicit halo
+    generator per rank (a random subset of its outer gids plus gids it does not hold, which
+    halo_generator skips, user_concepts.hpp:251-255): the product's reduced-halo make_pattern
+    (LoopbackWorld ranks) equals the oracle's all-ranks restatement, key for key."""
+    from tests.test_gpu_fuzz import draw_unstructured
+    from ghex_amd.context import LoopbackWorld
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
+    for seed in range(block * 25, block * 25 + 25):
+        case = draw_unstructured(seed)
+        nr = case["nr"]
+        by_rank = [[d for d in case["doms"] if d["rank"] == r] for r in range(nr)]
+        rng = np.random.default_rng(seed + 991)
+        hg = None
+        if seed % 2:
+            hg = []
+            for r in range(nr):
+                mult = {}  # each outer gid as often as the rank's first domain holding it has it
+                for d in by_rank[r]:
+                    cnt = {}
+                    for l in d["outer"]:
+                        cnt[d["gids"][l]] = cnt.get(d["gids"][l], 0) + 1
+                    for g, c in cnt.items():
+                        mult.setdefault(g, c)
+                pick = [g for g in sorted(mult) if rng.random() < 0.6 for _ in range(mult[g])]
+                pick += [7, 10 ** 6 + seed]
+                hg.append([int(x) for x in rng.permutation(pick)])
+        odoms = [[orc.UnstructuredDomain(d["id"], d["gids"], d["outer"]) for d in ds]
+                 for ds in by_rank]
+        try:
+            opats = orc.unstructured_make_pattern(
+                odoms, None if hg is None else [[hg[r]] * len(ds) for r, ds in enumerate(by_rank)])
+        except RuntimeError as e:  # e.g. a repeated gid only partly named: both must refuse
+            with pytest.raises(Exception, match=str(e)[:20]):
+                LoopbackWorld(nr).run(lambda ctx: make_pattern(
+                    ctx, HaloGenerator(hg[ctx.rank()]),
+                    [DomainDescriptor(d["id"], d["gids"], d["outer"]) for d in by_rank[ctx.rank()]]))
+            continue
+
+        def rank_fn(ctx):
+            r = ctx.rank()
+            mine = [DomainDescriptor(d["id"], d["gids"], d["outer"]) for d in by_rank[r]]
+            return make_pattern(ctx, HaloGenerator(None if hg is None else hg[r]), mine)
+
+        for r, pc in enumerate(LoopbackWorld(nr).run(rank_fn)):
+            for li in range(len(pc)):
+                for direction, key in ((0, "send"), (1, "recv")):
+                    got = [(rr, tag, rid, lids) for rid, rr, tag, lids in pc.halos(li, direction)]
+                    exp = [(rr, tag, rid, lids)
+                           for (rr, tag), (rid, lids) in opats[r][li][key].items()]
+                    assert got == exp, (seed, r, li, key)
