@@ -459,3 +459,28 @@ def test_unstructured_pattern_random_meshes_match_oracle(block):
                     exp = [(rr, tag, rid, lids)
                            for (rr, tag), (rid, lids) in opats[r][li][key].items()]
                     assert got == exp, (seed, r, li, key)
+
+
+def test_unstructured_pattern_edge_cases():
+    """A domain without outer cells, an explicit empty halo generator and a rank without any
+    halo: the reduced-halo make_pattern agrees with the oracle (empty maps where the reference
+    has none)."""
+    from ghex_amd.context import LoopbackWorld
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
+    ranks = [[(0, [10, 11, 12, 20, 21], [3, 4])],  # holds 20, 21 of rank 1 as outer cells
+             [(1, [20, 21, 22], [])]]              # no outer cells at all
+    for hgs in (None, [[21], []], [[], []]):
+        odoms = [[orc.UnstructuredDomain(i, g, o) for i, g, o in rs] for rs in ranks]
+        opats = orc.unstructured_make_pattern(
+            odoms, None if hgs is None else [[h] for h in hgs])
+
+        def rank_fn(ctx):
+            r = ctx.rank()
+            mine = [DomainDescriptor(i, g, o) for i, g, o in ranks[r]]
+            return make_pattern(ctx, HaloGenerator(None if hgs is None else hgs[r]), mine)
+
+        for r, pc in enumerate(LoopbackWorld(2).run(rank_fn)):
+            for direction, key in ((0, "send"), (1, "recv")):
+                got = [(rr, tag, rid, lids) for rid, rr, tag, lids in pc.halos(0, direction)]
+                exp = [(rr, tag, rid, lids) for (rr, tag), (rid, lids) in opats[r][0][key].items()]
+                assert got == exp, (hgs, r, key)
