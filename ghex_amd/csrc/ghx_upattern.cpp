@@ -274,8 +274,11 @@ int ghx_udomain_halo(const ghx_udomain* d, const int64_t* gen_gids, int64_t n_ge
         else d->make_outer_lids(gen_gids, n_gen, nullptr, &kept);
         *n_halo = int64_t(kept.size());
         if (int64_t(kept.size()) > cap) throw ghx::invalid("halo_gids: capacity too small");
-        if (!kept.empty()) need(halo_gids, "halo_gids");
-        std::memcpy(halo_gids, kept.data(), kept.size() * sizeof(int64_t));
+        if (!kept.empty())
+        {
+            need(halo_gids, "halo_gids");
+            std::memcpy(halo_gids, kept.data(), kept.size() * sizeof(int64_t));
+        }
         return GHX_OK;
     });
 }

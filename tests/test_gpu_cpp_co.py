@@ -63,7 +63,7 @@ def test_co_loopback_all_gather_cpu(tmp_path):
     assert subprocess.run([str(exe)], timeout=60).returncode == 0
 
 
-def test_co_unstructured_make_pattern_known_answer_cpu(tmp_path, golden_dir):
+def test_co_unstructured_make_pattern_compiles_known_answer_cpu(tmp_path, golden_dir):
     """The C++ make_pattern<unstructured> (reduced halos through the transport's all_gather) on
     4 loopback threads, no GPU: every rank's send/recv lid tables equal the reference's
     known-answer tables (unstructured_test_case.hpp:217-343)."""
