@@ -15,20 +15,24 @@
 // the indices resident in device memory (the reference reads them from managed memory).
 //
 // Plans: the first pack/unpack of an index list uploads it once (ghx_uplan_create); later calls
-// with the same list find the plan by the list's address, length and index width, O(1) host
-// work per call. This relies on the reference's contract that the pattern's index containers are
-// immutable and outlive every exchange that uses them (include/ghex/pattern_container.hpp:84-87);
-// call forget_plans() after changing a list in place. (The plain C entry points
-// ghx_unstructured_pack/unpack compare the whole list on every call instead.)
+// with the same list find the plan by the list's address, length and index width and check 16
+// sampled entries (O(1) host work per call; a list rebuilt at the same address, e.g. by a new
+// pattern, differs there almost surely and gets a new plan). This relies on the reference's
+// contract that the pattern's index containers are immutable and outlive every exchange that
+// uses them (include/ghex/pattern_container.hpp:84-87); call forget_plans() after changing a list
+// in place. Copies of a descriptor share its plans (guarded by a mutex). (The plain C entry
+// points ghx_unstructured_pack/unpack compare the whole list on every call instead.)
 //
 // Depends only on <ghx.h> and the standard library; link with -lghx.
 #pragma once
 
 #include <ghx.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -65,8 +69,18 @@ class data_descriptor
     ghx_udata_desc m_desc{};
     // (list address, length, index bytes, direction) -> plan; shared by copies of the descriptor
     using plan_key = std::tuple<const void*, std::size_t, int32_t, int32_t>;
-    using plan_map = std::map<plan_key, std::shared_ptr<ghx_uplan>>;
-    std::shared_ptr<plan_map> m_plans = std::make_shared<plan_map>();
+    static constexpr int kSamples = 16;
+    struct cached
+    {
+        std::shared_ptr<ghx_uplan> plan;
+        int64_t sample[kSamples];  // entries at i * (n - 1) / (kSamples - 1)
+    };
+    struct plan_cache
+    {
+        std::mutex mtx;
+        std::map<plan_key, cached> map;
+    };
+    std::shared_ptr<plan_cache> m_plans = std::make_shared<plan_cache>();
 
   public:
     /** values: device pointer to domain_size * levels elements (plus padding when
@@ -123,7 +137,11 @@ class data_descriptor
     }
 
     // drop the cached plans (after an index list was changed in place)
-    void forget_plans() { m_plans->clear(); }
+    void forget_plans()
+    {
+        std::lock_guard<std::mutex> g(m_plans->mtx);
+        m_plans->map.clear();
+    }
 
   private:
     template<typename V>
@@ -131,24 +149,41 @@ class data_descriptor
     {
         if (l.empty()) return;
         const plan_key key{static_cast<const void*>(l.data()), l.size(), lid_bytes(l), dir};
-        auto it = m_plans->find(key);
-        if (it == m_plans->end())
+        int64_t sample[kSamples];
+        for (int i = 0; i < kSamples; ++i)
+            sample[i] = int64_t(l[(l.size() - 1) * std::size_t(i) / (kSamples - 1)]);
+        std::shared_ptr<ghx_uplan> plan;  // held: a concurrent forget_plans() cannot free it
         {
-            std::vector<int64_t> wide(l.begin(), l.end());
-            ghx_upack_entry e{};
-            e.data = m_desc;
-            e.field_slot = 0;
-            e.buffer_slot = 0;
-            e.buffer_offset = 0;
-            e.lids = wide.data();
-            e.n_lids = int64_t(wide.size());
-            ghx_uplan* p = nullptr;
-            check_u(ghx_uplan_create(&e, 1, dir, &p), "ghx_uplan_create");
-            it = m_plans->emplace(key, std::shared_ptr<ghx_uplan>(p, ghx_uplan_destroy)).first;
+            std::lock_guard<std::mutex> g(m_plans->mtx);
+            auto it = m_plans->map.find(key);
+            if (it != m_plans->map.end() &&
+                !std::equal(sample, sample + kSamples, it->second.sample))
+            {
+                m_plans->map.erase(it);  // a different list at the same address
+                it = m_plans->map.end();
+            }
+            if (it == m_plans->map.end())
+            {
+                std::vector<int64_t> wide(l.begin(), l.end());
+                ghx_upack_entry e{};
+                e.data = m_desc;
+                e.field_slot = 0;
+                e.buffer_slot = 0;
+                e.buffer_offset = 0;
+                e.lids = wide.data();
+                e.n_lids = int64_t(wide.size());
+                ghx_uplan* p = nullptr;
+                check_u(ghx_uplan_create(&e, 1, dir, &p), "ghx_uplan_create");
+                cached c;
+                c.plan.reset(p, ghx_uplan_destroy);
+                std::copy(sample, sample + kSamples, c.sample);
+                it = m_plans->map.emplace(key, std::move(c)).first;
+            }
+            plan = it->second.plan;
         }
         void* f[1] = {m_values};
         void* b[1] = {buffer};
-        check_u(ghx_uplan_execute(it->second.get(), f, 1, b, 1, stream_of(stream_ptr)),
+        check_u(ghx_uplan_execute(plan.get(), f, 1, b, 1, stream_of(stream_ptr)),
                 dir ? "unpack: ghx_uplan_execute" : "pack: ghx_uplan_execute");
     }
 

@@ -3,11 +3,13 @@
 // &stream) of one neighbour's index list, then unpack(...) of a received buffer.
 // Usage: udata_demo n_cells levels levels_first lid_bytes(4|8) lids_file out_prefix
 //   lids_file: int64 local indices; values[i, l] = i*100 + l before the pack;
-//   writes <out>.buf (packed buffer) and <out>.values (after unpacking buffer[k] = 1e6 + k).
+//   writes <out>.buf (packed buffer), <out>.values (after unpacking buffer[k] = 1e6 + k) and
+//   <out>.buf2 (the list reversed in place, packed again from those values).
 #include <hip/hip_runtime.h>
 
 #include <ghex_amd/data_descriptor.hpp>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -61,6 +63,14 @@ int run(size_t n, int levels, bool lf, const std::vector<int64_t>& lids, const c
     HCK(hipMemcpy(host.data(), values, host.size() * 8, hipMemcpyDeviceToHost));
     std::ofstream(std::string(out) + ".values", std::ios::binary)
         .write(reinterpret_cast<const char*>(host.data()), std::streamsize(host.size() * 8));
+    // a different list at the same address (same length): the adaptor's sampled check must
+    // build a new plan, so this pack gathers in the reversed order
+    std::reverse(c[0].m_lids.begin(), c[0].m_lids.end());
+    d.pack(buf, c, &s);
+    HCK(hipStreamSynchronize(s));
+    HCK(hipMemcpy(hb.data(), buf, nb * 8, hipMemcpyDeviceToHost));
+    std::ofstream(std::string(out) + ".buf2", std::ios::binary)
+        .write(reinterpret_cast<const char*>(hb.data()), std::streamsize(nb * 8));
     HCK(hipFree(values));
     HCK(hipFree(buf));
     HCK(hipStreamDestroy(s));

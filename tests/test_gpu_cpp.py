@@ -84,3 +84,7 @@ def test_cpp_unstructured_adaptor(tmp_path, levels, levels_first, lid_bytes):
     exp = vals.copy()
     orc.unstructured_set(exp, rb.view(np.uint8), 8, lids, levels, levels_first, isd, lsd)
     np.testing.assert_array_equal(np.fromfile(pre + ".values", dtype=np.float64), exp)
+    # the list reversed in place at the same address: a new plan, not the cached one
+    ob2 = np.zeros(len(lids) * levels * 8, np.uint8)
+    orc.unstructured_get(exp, ob2, 8, lids[::-1].copy(), levels, levels_first, isd, lsd)
+    np.testing.assert_array_equal(np.fromfile(pre + ".buf2", dtype=np.uint8), ob2)
