@@ -214,3 +214,29 @@ def test_config5_pattern_full_size_gloo_two_ranks():
 
 def test_config5_pattern_four_ranks_gloo():
     _run(4, _config5_worker, 200_000)
+
+
+def _multi_domain_worker(rank, world, case, grouping):
+    import ghex_amd
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
+    d = case["domains"]
+    mine = [DomainDescriptor(i, d[str(i)]["gids"], d[str(i)]["halo_lids"]) for i in grouping[rank]]
+    pc = make_pattern(ghex_amd.make_context(), HaloGenerator(), mine)
+    odoms = [[orc.UnstructuredDomain(i, d[str(i)]["gids"], d[str(i)]["halo_lids"]) for i in g]
+             for g in grouping]
+    opats = orc.unstructured_make_pattern(odoms)
+    for li in range(len(grouping[rank])):
+        for direction, key in ((0, "send"), (1, "recv")):
+            got = [(rr, tag, rid, lids) for rid, rr, tag, lids in pc.halos(li, direction)]
+            exp = [(rr, tag, rid, lids) for (rr, tag), (rid, lids) in opats[rank][li][key].items()]
+            assert got == exp, (li, key, got, exp)
+
+
+def test_unstructured_multi_domain_ranks_gloo(golden_dir):
+    """Two gloo ranks with two domains each (the known-answer case): the setup's
+    point-to-point gid lists include messages a rank sends itself (between its two domains),
+    which Context.exchange_arrays keeps local; patterns equal the oracle's."""
+    import json
+    with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
+        case = json.load(fh)
+    _run(2, _multi_domain_worker, case, [[0, 1], [2, 3]])
