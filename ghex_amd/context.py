@@ -71,6 +71,37 @@ class Context:
         self._dist.all_gather(outs, t, group=self.group)
         return [o[:k].cpu().numpy() for o, k in zip(outs, sizes)]
 
+    def ring_arrays(self, arr):
+        """The reference's distributed_for_each (include/ghex/mpi/communicator.hpp:233-345):
+        yields (rank, that rank's int64 array) for every rank, this rank's first, then passing
+        the arrays around a ring (send to rank-1, receive from rank+1), so at most two arrays are
+        held at a time (every rank must consume the whole generator)."""
+        import numpy as np
+        arr = np.ascontiguousarray(arr, dtype=np.int64)
+        me, w = self.rank(), self.size()
+        if self._dist is None or w == 1:
+            yield me, arr
+            return
+        import torch
+        dist, dev = self._dist, self._collective_device()
+        m = torch.tensor([arr.size], dtype=torch.int64, device=dev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
+        cap = int(m.item()) + 1
+        buf = torch.zeros(cap, dtype=torch.int64, device=dev)
+        buf[0] = arr.size
+        buf[1:1 + arr.size] = torch.from_numpy(arr).to(dev)
+        left, right = self.global_rank((me - 1) % w), self.global_rank((me + 1) % w)
+        for step in range(w):
+            n = int(buf[0].item())
+            yield (me + step) % w, buf[1:1 + n].cpu().numpy()
+            if step < w - 1:
+                nxt = torch.empty(cap, dtype=torch.int64, device=dev)
+                ops = [dist.P2POp(dist.isend, buf, left, self.group),
+                       dist.P2POp(dist.irecv, nxt, right, self.group)]
+                for wk in dist.batch_isend_irecv(ops):
+                    wk.wait()
+                buf = nxt
+
     def exchange_arrays(self, sends, recvs):
         """Setup-time point-to-point: sends = [(dst rank, int64 array)], recvs = [(src rank,
         length)]; returns the received arrays in `recvs` order. Messages of one (src, dst) pair
@@ -244,6 +275,12 @@ class LoopbackContext:
     def all_gather_array(self, arr):
         import numpy as np
         return self.all_gather_object(np.ascontiguousarray(arr, dtype=np.int64))
+
+    def ring_arrays(self, arr):
+        every = self.all_gather_array(arr)
+        for step in range(self._w.n):
+            r = (self._r + step) % self._w.n
+            yield r, every[r]
 
     def exchange_arrays(self, sends, recvs):
         import numpy as np

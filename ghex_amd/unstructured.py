@@ -79,8 +79,9 @@ def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[Domain
     exchange their domains' halo gids (never their full gid lists), each rank resolves every
     halo against its own inner gids (its send halos) and ships the gids it found back to the
     halo's owner, which turns them into outer local ids (its receive halos). Collectives:
-    `context.all_gather_object` (ids, record metadata), `context.all_gather_array` (reduced
-    halos), `context.exchange_arrays` (gid lists, point to point)."""
+    `context.all_gather_object` (ids, record metadata), `context.ring_arrays` (reduced halos,
+    the reference's distributed_for_each ring), `context.exchange_arrays` (gid lists, point to
+    point)."""
     import numpy as np
     doms = list(domain_range)
     if not doms:
@@ -100,8 +101,9 @@ def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[Domain
         payload = np.concatenate([np.array([len(doms)], np.int64), np.array(ids, np.int64),
                                   np.array([h.size for h in halos], np.int64)] + halos)
         n_rec = ctypes.c_int64()
-        # every rank's reduced halos against my inner gids -> send halos (:284-330)
-        for r, arr in enumerate(context.all_gather_array(payload)):
+        # every rank's reduced halos, around the ring, against my inner gids -> send halos
+        # (:284-330; at most two ranks' halos held at a time)
+        for r, arr in context.ring_arrays(payload):
             k = int(arr[0])
             rid = np.ascontiguousarray(arr[1:1 + k], dtype=np.int32)
             sizes = np.ascontiguousarray(arr[1 + k:1 + 2 * k])
