@@ -1039,7 +1039,45 @@ def _floor_lib():
     L.ghx_probe_fused_floor.restype = ctypes.c_int
     L.ghx_probe_fused_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_double)]
+    P32 = ctypes.POINTER(ctypes.c_int32)
+    L.ghx_probe_index_floor.restype = ctypes.c_int
+    L.ghx_probe_index_floor.argtypes = [ctypes.c_int64, ctypes.c_int, P32, ctypes.c_int64, P32,
+                                        ctypes.c_int64, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double)]
     return L
+
+
+def index_floor(cells, levels, sends, recvs, k_gather, k_scatter):
+    """Config 5's index-list floor (tools/pack_floor.hip ghx_probe_index_floor): the simplest
+    gather / scatter kernels over the same lid lists (one value per lane, no plan), timed by their
+    own begin/end events like the product's launches (k_gather / k_scatter, seconds).
+    floor_over_kernel = probe time / product time (above 1: the product is faster)."""
+    import ctypes
+
+    import numpy as np
+    try:
+        L = _floor_lib()
+        if L is None:
+            return {"error": "tools/lib/libpackfloor.so not built (make -C tools)"}
+        sl = np.ascontiguousarray(np.concatenate([l for *_, l in sends]), dtype=np.int32)
+        rl = np.ascontiguousarray(np.concatenate([l for *_, l in recvs]), dtype=np.int32)
+        us = (ctypes.c_double * 4)()
+        P32 = ctypes.POINTER(ctypes.c_int32)
+        rc = L.ghx_probe_index_floor(cells, levels, sl.ctypes.data_as(P32), sl.size,
+                                     rl.ctypes.data_as(P32), rl.size, 21, us)
+        if rc:
+            return {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
+        return {"gather_us": round(us[0], 2), "scatter_us": round(us[2], 2),
+                "gather_cold_us": round(us[1], 2), "scatter_cold_us": round(us[3], 2),
+                "pack_kernel_us": round(k_gather * 1e6, 2),
+                "unpack_kernel_us": round(k_scatter * 1e6, 2),
+                "gather_floor_over_kernel": round(us[0] / (k_gather * 1e6), 3) if k_gather else None,
+                "scatter_floor_over_kernel": round(us[2] / (k_scatter * 1e6), 3)
+                if k_scatter else None,
+                "what": "the simplest gather / scatter kernels over the same lid lists (one fp64 "
+                        "value per lane, no plan), kernel-own events, medians of 21"}
+    except Exception as e:  # reported, never fatal
+        return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
 
 
 def fused_floor(N, Hw, launch_us):
@@ -1696,6 +1734,14 @@ def bench_config5(torch, dev, _ghx, levels, pats, cpu_seconds=None):
         exp = torch.from_numpy(np.ascontiguousarray(host[l])).to(dev).view(-1)
         bad += int((b.view(torch.float64) != exp).sum().item())
     del keep
+    # the two launches by their own events, beside the index-list floor probe
+    def gather(st):
+        _ghx.check(L.ghx_uplan_execute(hp, fp, 1, sp, len(sbufs), st), "uplan pack")
+
+    def scatter(st):
+        _ghx.check(L.ghx_uplan_execute(hu, fp, 1, rp, len(rbufs), st), "uplan unpack")
+    k_g, k_s = launch_durations(torch, dev, torch.cuda.current_stream(dev), _ghx,
+                                [gather, scatter])
     n_send = sum(len(l) for *_, l in sends)
     n_recv = sum(len(l) for *_, l in recvs)
     nbytes = 2 * (n_send + n_recv) * levels * 8
@@ -1709,7 +1755,8 @@ def bench_config5(torch, dev, _ghx, levels, pats, cpu_seconds=None):
                             "buffers set to 0xFF, outer cells to -1, receive buffers holding each "
                             "peer's packed send list; every send value and every cell checked",
            "inputs": "rank 0 of 8 (tools/config5_gen.cpp), lists from the product's "
-                     "make_pattern<unstructured> with the 8 ranks as threads"}
+                     "make_pattern<unstructured> with the 8 ranks as threads",
+           "index_floor": index_floor(int(n), levels, sends, recvs, k_g, k_s)}
     if cpu_seconds:
         res["cpu_baseline"] = cpu_baseline_config5(cpu_seconds, host, sends, recvs, peer_bytes,
                                                    [b.cpu().numpy() for b in sbufs], levels)

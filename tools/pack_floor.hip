@@ -388,6 +388,92 @@ done:
     return rc;
 }
 
+
+// Config 5's index-list floor (round 5): the simplest gather and scatter of the SAME lid lists
+// the product runs (levels-first rows of `levels` fp64 values): one (lid, level) value per lane,
+// buffer side lane-linear, no plan, no run detection, no tiles. What the memory system takes for
+// those random rows; bench.py sets it beside the product's fused launches (floor_over_kernel).
+__global__ __launch_bounds__(256) void k_igather(const double* __restrict__ f, const int* __restrict__ lids,
+                                                 double* __restrict__ buf, uint64_t n, int L)
+{
+    for (uint64_t k = uint64_t(blockIdx.x) * 256 + threadIdx.x; k < n * uint64_t(L);
+         k += uint64_t(gridDim.x) * 256)
+        buf[k] = f[uint64_t(lids[k / L]) * L + k % L];
+}
+
+__global__ __launch_bounds__(256) void k_iscatter(double* __restrict__ f, const int* __restrict__ lids,
+                                                  const double* __restrict__ buf, uint64_t n, int L)
+{
+    for (uint64_t k = uint64_t(blockIdx.x) * 256 + threadIdx.x; k < n * uint64_t(L);
+         k += uint64_t(gridDim.x) * 256)
+        f[uint64_t(lids[k / L]) * L + k % L] = buf[k];
+}
+
+// out_us[4]: {gather, scatter} x {warm, cold} (kernel-own events, median of reps).
+extern "C" int ghx_probe_index_floor(int64_t cells, int levels, const int32_t* send_lids,
+                                     int64_t n_send, const int32_t* recv_lids, int64_t n_recv,
+                                     int reps, double* out_us)
+{
+    int rc = 0;
+    const size_t flush_bytes = size_t(1) << 30;
+    double *field = nullptr, *sbuf = nullptr, *rbuf = nullptr;
+    int *d_s = nullptr, *d_r = nullptr;
+    char* fl = nullptr;
+    unsigned* sink = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const int grid = 256 * 16;
+    const int L = levels;
+    CK(hipMalloc(&field, size_t(cells) * L * 8));
+    CK(hipMalloc(&sbuf, size_t(n_send) * L * 8 + 8));
+    CK(hipMalloc(&rbuf, size_t(n_recv) * L * 8 + 8));
+    CK(hipMalloc(&d_s, size_t(n_send) * 4 + 4));
+    CK(hipMalloc(&d_r, size_t(n_recv) * 4 + 4));
+    CK(hipMalloc(&fl, flush_bytes));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemcpy(d_s, send_lids, size_t(n_send) * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_r, recv_lids, size_t(n_recv) * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(field, 1, size_t(cells) * L * 8));
+    CK(hipMemset(rbuf, 2, size_t(n_recv) * L * 8 + 8));
+    CK(hipMemset(fl, 3, flush_bytes));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int j = 0; j < 2; ++j)
+        for (int cold = 0; cold < 2; ++cold)
+        {
+            std::vector<float> t;
+            auto launch = [&](hipEvent_t a, hipEvent_t b) {
+                if (j == 0)
+                    hipExtLaunchKernelGGL(k_igather, dim3(grid), dim3(256), 0, 0, a, b, 0,
+                                          (const double*)field, (const int*)d_s, sbuf,
+                                          uint64_t(n_send), L);
+                else
+                    hipExtLaunchKernelGGL(k_iscatter, dim3(grid), dim3(256), 0, 0, a, b, 0, field,
+                                          (const int*)d_r, (const double*)rbuf, uint64_t(n_recv), L);
+            };
+            for (int i = 0; i < reps; ++i)
+            {
+                if (cold)
+                    hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, 0, (const v4*)fl,
+                                       flush_bytes / 16, sink);
+                else
+                    launch(nullptr, nullptr);
+                launch(e0, e1);
+                CK(hipEventSynchronize(e1));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                t.push_back(ms * 1e3f);
+            }
+            std::sort(t.begin(), t.end());
+            out_us[2 * j + cold] = t[t.size() / 2];
+        }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    for (void* p : {(void*)field, (void*)sbuf, (void*)rbuf, (void*)d_s, (void*)d_r, (void*)fl, (void*)sink})
+        if (p) (void)hipFree(p);
+    return rc;
+}
+
 #ifdef PACK_FLOOR_MAIN
 int main(int argc, char** argv)
 {

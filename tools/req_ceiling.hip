@@ -65,6 +65,38 @@ __global__ __launch_bounds__(256) void k_write_pieces(char* p, size_t n, size_t 
         *(v4*)(p + i * stride) = v4{unsigned(i), 1, 2, 3};
 }
 
+// config 5's shapes in their simplest form (round 5): one int32 index per lane (coalesced), one
+// 8-B access at field + index * 8 (a random line of an 84 MB field), with or without the
+// lane-linear buffer side of a gather / scatter
+__global__ __launch_bounds__(256) void k_read_random(const double* f, const int* idx, size_t n,
+                                                     unsigned* sink)
+{
+    double acc = 0;
+    for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += size_t(gridDim.x) * 256)
+        acc += f[idx[i]];
+    if (acc == 1.2345) sink[0] = 1;
+}
+
+__global__ __launch_bounds__(256) void k_write_random(double* f, const int* idx, size_t n)
+{
+    for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += size_t(gridDim.x) * 256)
+        f[idx[i]] = double(i);
+}
+
+__global__ __launch_bounds__(256) void k_gather_random(const double* f, const int* idx,
+                                                       double* buf, size_t n)
+{
+    for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += size_t(gridDim.x) * 256)
+        buf[i] = f[idx[i]];
+}
+
+__global__ __launch_bounds__(256) void k_scatter_random(double* f, const int* idx,
+                                                        const double* buf, size_t n)
+{
+    for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += size_t(gridDim.x) * 256)
+        f[idx[i]] = buf[i];
+}
+
 int main(int argc, char** argv)
 {
     const int reps = argc > 1 ? atoi(argv[1]) : 11;
@@ -130,6 +162,44 @@ int main(int argc, char** argv)
         snprintf(name, sizeof name, "write_pieces_stride%zu", stride);
         report(name, 0, double(n), double(n) * 16,
                [&] { hipLaunchKernelGGL(k_write_pieces, dim3(grid), dim3(256), 0, 0, f, n, stride); });
+    }
+    {
+        // config 5 (round 5): 500k distinct random cells of a 10.5M-cell fp64 field (84 MB)
+        const size_t cells = 10500000, n = 500000;
+        std::vector<int> h(cells);
+        for (size_t i = 0; i < cells; ++i) h[i] = int(i);
+        unsigned long long x = 20260715ull;
+        for (size_t i = cells - 1; i > 0; --i)  // Fisher-Yates with splitmix64
+        {
+            x += 0x9e3779b97f4a7c15ull;
+            unsigned long long z = x;
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+            z ^= z >> 31;
+            std::swap(h[i], h[size_t(z % (i + 1))]);
+        }
+        int* idx;
+        double* buf;
+        CK(hipMalloc(&idx, 2 * n * sizeof(int)));  // [0, n): gather cells, [n, 2n): scatter cells
+        CK(hipMalloc(&buf, n * sizeof(double)));
+        CK(hipMemcpy(idx, h.data(), 2 * n * sizeof(int), hipMemcpyHostToDevice));
+        CK(hipMemset(buf, 0, n * sizeof(double)));
+        const double* fd = (const double*)f;
+        report("read_random_8B_of_84MB", double(n), 0, double(n) * 8,
+               [&] { hipLaunchKernelGGL(k_read_random, dim3(grid), dim3(256), 0, 0, fd, idx, n, sink); });
+        report("write_random_8B_of_84MB", 0, double(n), double(n) * 8,
+               [&] { hipLaunchKernelGGL(k_write_random, dim3(grid), dim3(256), 0, 0, (double*)f, idx, n); });
+        report("gather_random_8B_of_84MB", double(n), double(n) / 8, double(n) * 16,
+               [&] { hipLaunchKernelGGL(k_gather_random, dim3(grid), dim3(256), 0, 0, fd, idx, buf, n); });
+        report("scatter_random_8B_of_84MB", double(n) / 16, double(n), double(n) * 16,
+               [&] { hipLaunchKernelGGL(k_scatter_random, dim3(grid), dim3(256), 0, 0, (double*)f, idx, buf, n); });
+        report("gather_then_scatter_random_8B_of_84MB", double(n) * 17 / 16, double(n) * 9 / 8,
+               double(n) * 32, [&] {
+                   hipLaunchKernelGGL(k_gather_random, dim3(grid), dim3(256), 0, 0, fd, idx, buf, n);
+                   hipLaunchKernelGGL(k_scatter_random, dim3(grid), dim3(256), 0, 0, (double*)f, idx + n, buf, n);
+               });
+        CK(hipFree(idx));
+        CK(hipFree(buf));
     }
     CK(hipFree(a));
     CK(hipFree(b));
