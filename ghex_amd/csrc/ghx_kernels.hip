@@ -170,41 +170,12 @@ __device__ __forceinline__ int64_t load_lid(const seg_u& s, uint32_t i)
     return ((const GHX_GLOBAL int32_t*)(s.lids))[i];
 }
 
-// field byte offset of segment-relative buffer position p (unstructured: rows from lids)
-__device__ __forceinline__ int64_t field_offset_u(const seg_u& s, uint32_t p)
-{
-    const uint32_t row = fastdiv(p, s.mag_row);
-    const uint32_t col = p - row * s.row_bytes;
-    uint32_t i, l;
-    if (s.mode == 0)
-    {
-        i = row;
-        l = 0;
-    }
-    else if (s.mode == 1)
-    {
-        i = fastdiv(row, s.mag_inner);
-        l = row - i * s.row_levels;
-    }
-    else
-    {
-        l = fastdiv(row, s.mag_inner);
-        i = row - l * s.n;
-    }
-    return s.field_off + load_lid(s, i) * s.index_stride_b + int64_t(l) * s.level_stride_b + int64_t(col);
-}
-
 template<typename Seg>
 __device__ __forceinline__ int64_t field_offset(const Seg& s, uint32_t p);
 template<>
 __device__ __forceinline__ int64_t field_offset<seg_s>(const seg_s& s, uint32_t p)
 {
     return field_offset_s(s, p);
-}
-template<>
-__device__ __forceinline__ int64_t field_offset<seg_u>(const seg_u& s, uint32_t p)
-{
-    return field_offset_u(s, p);
 }
 
 // Copy one tile [start, end) of a segment. Lane-linear in buffer space: lanes of a wave touch
@@ -413,7 +384,123 @@ __device__ __forceinline__ int ptr_wlog2(uint64_t p)
     return __builtin_ctzll(p | 16ull);  // log2 of the largest power of two (<= 16) dividing p
 }
 
-template<bool PACK, typename Seg>
+// Unstructured tile, general path (rows that are not 4/8-B runs, e.g. config 5's 64-B
+// levels-first rows): all kU index loads of a lane, then all kU value loads, are issued
+// together. Written branch-free per vector: the uniform choices (index width, row mode, cache
+// policy) are hoisted out of the per-vector code, and a vector position past the tile's end is
+// clamped to the tile's last vector, which moves the same bytes again (a duplicate store of
+// identical bytes by another lane of this workgroup). Per-vector branches made the compiler wait
+// for each index load before issuing the next (s_waitcnt vmcnt(0) inside every branch): four
+// dependent round trips per lane instead of one.
+template<bool PACK, int W, int kU>
+__device__ __forceinline__ void copy_tile_u(const seg_u& s, char* __restrict__ field,
+                                            char* __restrict__ buf, uint32_t start, uint32_t end)
+{
+    using V = typename vec_t<W>::type;
+    const uint32_t last = end - W;  // tiles hold whole rows: end - start is a multiple of W
+    const uint32_t pol = s.fpol;
+    for (uint32_t base = start + threadIdx.x * W; base < end; base += kU * kBlock * W)
+    {
+        uint32_t p[kU], idx[kU];
+        int64_t extra[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) p[u] = min(base + uint32_t(u) * kBlock * W, last);
+        V v[kU];
+        if (!PACK)
+        {
+#pragma unroll
+            for (int u = 0; u < kU; ++u) v[u] = vload<V>(buf + p[u]);
+        }
+        if (s.mode == 0)
+        {
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+            {
+                const uint32_t row = fastdiv(p[u], s.mag_row);
+                idx[u] = row;
+                extra[u] = int64_t(p[u] - row * s.row_bytes);
+            }
+        }
+        else if (s.mode == 1)
+        {
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+            {
+                const uint32_t row = fastdiv(p[u], s.mag_row);
+                const uint32_t i = fastdiv(row, s.mag_inner);
+                idx[u] = i;
+                extra[u] = int64_t(row - i * s.row_levels) * s.level_stride_b +
+                           int64_t(p[u] - row * s.row_bytes);
+            }
+        }
+        else
+        {
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+            {
+                const uint32_t row = fastdiv(p[u], s.mag_row);
+                const uint32_t l = fastdiv(row, s.mag_inner);
+                idx[u] = row - l * s.n;
+                extra[u] = int64_t(l) * s.level_stride_b + int64_t(p[u] - row * s.row_bytes);
+            }
+        }
+        int64_t lid[kU];
+        if (s.lid64)
+        {
+#pragma unroll
+            for (int u = 0; u < kU; ++u) lid[u] = ((const GHX_GLOBAL int64_t*)(s.lids))[idx[u]];
+        }
+        else
+        {
+#pragma unroll
+            for (int u = 0; u < kU; ++u) lid[u] = ((const GHX_GLOBAL int32_t*)(s.lids))[idx[u]];
+        }
+        int64_t fo[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) fo[u] = s.field_off + lid[u] * s.index_stride_b + extra[u];
+        if (PACK)
+        {
+            if (pol & 1u)
+            {
+#pragma unroll
+                for (int u = 0; u < kU; ++u) v[u] = fload<V>(field + fo[u], 1u);
+            }
+            else
+            {
+#pragma unroll
+                for (int u = 0; u < kU; ++u) v[u] = vload<V>(field + fo[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) vstore<V>(buf + p[u], v[u]);
+        }
+        else if (pol & 2u)
+        {
+#pragma unroll
+            for (int u = 0; u < kU; ++u) fstore<V>(field + fo[u], v[u], 2u);
+        }
+        else
+        {
+#pragma unroll
+            for (int u = 0; u < kU; ++u) vstore<V>(field + fo[u], v[u]);
+        }
+    }
+}
+
+template<bool PACK, int UU>
+__device__ __forceinline__ void copy_any(const seg_u& s, char* field, char* buf, uint32_t start,
+                                         uint32_t end, int w)
+{
+    switch (w)
+    {
+        case 4: copy_tile_u<PACK, 16, UU>(s, field, buf, start, end); break;
+        case 3: copy_tile_u<PACK, 8, UU>(s, field, buf, start, end); break;
+        case 2: copy_tile_u<PACK, 4, UU>(s, field, buf, start, end); break;
+        case 1: copy_tile_u<PACK, 2, UU>(s, field, buf, start, end); break;
+        default: copy_tile_u<PACK, 1, UU>(s, field, buf, start, end); break;
+    }
+}
+
+template<bool PACK, int UU, typename Seg>
 __device__ __forceinline__ void copy_any(const Seg& s, char* field, char* buf, uint32_t start,
                                          uint32_t end, int w)
 {
@@ -439,7 +526,7 @@ __device__ __forceinline__ bool odd_parity(const kargs& a)
              a.parity_add) & 1) != 0;
 }
 
-template<bool PACK, typename Seg, bool RUNS = false, bool DBL = false>
+template<bool PACK, typename Seg, bool RUNS = false, bool DBL = false, int UU = kU>
 __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
 {
     const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
@@ -465,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         int w = s.wlog2;
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
-        copy_any<PACK>(s, field, buf, start, end, w);
+        copy_any<PACK, UU>(s, field, buf, start, end, w);
     }
 }
 
@@ -548,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
         if (q.bytes == 0)
         {
             // a peer message of a mixed exchange (ghx_exchange_pack_self): pack only
-            copy_any<true>(s, field_p, buf, start, end, wp);
+            copy_any<true, kU>(s, field_p, buf, start, end, wp);
             continue;
         }
         if (wp == wu)
@@ -563,9 +650,9 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
             }
             continue;
         }
-        copy_any<true>(s, field_p, buf, start, end, wp);
+        copy_any<true, kU>(s, field_p, buf, start, end, wp);
         __syncthreads();  // workgroup release/acquire: the tile's buffer bytes are complete
-        copy_any<false>(q, field_u, buf, start, end, wu);
+        copy_any<false, kU>(q, field_u, buf, start, end, wu);
         __syncthreads();  // the next tile of a grid-stride loop reuses the lanes
     }
 }
@@ -721,6 +808,24 @@ int launch_put(const kargs& a, void* stream, uint32_t grid)
     return launched("put");
 }
 
+template<bool DBL, int UU>
+void launch_u_general(const kargs& a, int direction, hipStream_t s, uint32_t grid)
+{
+    if (direction == 0) launch((k_copy<true, seg_u, false, DBL, UU>), grid, s, a);
+    else launch((k_copy<false, seg_u, false, DBL, UU>), grid, s, a);
+}
+
+template<bool DBL>
+void launch_u_general(const kargs& a, int direction, hipStream_t s, uint32_t grid)
+{
+    switch (g_tune.u_unroll)
+    {
+        case 1: launch_u_general<DBL, 1>(a, direction, s, grid); break;
+        case 2: launch_u_general<DBL, 2>(a, direction, s, grid); break;
+        default: launch_u_general<DBL, 4>(a, direction, s, grid); break;
+    }
+}
+
 int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid, bool runs)
 {
     if (a.n_tiles == 0) return GHX_OK;
@@ -729,13 +834,11 @@ int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t gr
     {
         if (runs && direction == 0) launch((k_copy<true, seg_u, true, true>), grid, s, a);
         else if (runs) launch((k_copy<false, seg_u, true, true>), grid, s, a);
-        else if (direction == 0) launch((k_copy<true, seg_u, false, true>), grid, s, a);
-        else launch((k_copy<false, seg_u, false, true>), grid, s, a);
+        else launch_u_general<true>(a, direction, s, grid);
     }
     else if (runs && direction == 0) launch((k_copy<true, seg_u, true>), grid, s, a);
     else if (runs) launch((k_copy<false, seg_u, true>), grid, s, a);
-    else if (direction == 0) launch((k_copy<true, seg_u>), grid, s, a);
-    else launch((k_copy<false, seg_u>), grid, s, a);
+    else launch_u_general<false>(a, direction, s, grid);
     return launched("unstructured");
 }
 

@@ -83,6 +83,14 @@ uint32_t short_tile_rows(const seg_u& s, uint64_t)
 {
     return s.runs == 2 ? g_tune.u_run_tile_rows : g_tune.u_tile_rows;
 }
+// tile of segments with long rows: structured / unstructured
+uint32_t long_tile_bytes(const seg_s&) { return g_tune.tile_bytes; }
+uint32_t long_tile_bytes(const seg_u& s)
+{
+    // whole rows per tile (at least one)
+    const uint32_t tb = std::max<uint32_t>(g_tune.u_tile_bytes, s.row_bytes);
+    return tb - tb % s.row_bytes;
+}
 
 // Tile table: per tile {segment, tile index within the segment}. Segments with short rows
 // (request-bound: one memory request per row) may use a different tile size from streaming
@@ -97,7 +105,7 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
         const bool small = segs[i].row_bytes < g_tune.small_row_bytes;
-        uint32_t tb = g_tune.tile_bytes;
+        uint32_t tb = long_tile_bytes(segs[i]);
         if (small)
         {
             const uint32_t rows = short_tile_rows(segs[i], short_rows);

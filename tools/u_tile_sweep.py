@@ -12,13 +12,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SETTINGS = [
-    {},
-    {"tile_bytes": 4096}, {"tile_bytes": 16384}, {"tile_bytes": 32768}, {"tile_bytes": 65536},
-    {"small_row_bytes": 65, "u_tile_rows": 64}, {"small_row_bytes": 65, "u_tile_rows": 128},
-    {"small_row_bytes": 65, "u_tile_rows": 256}, {"small_row_bytes": 65, "u_tile_rows": 512},
-    {"grid_cap": 2048}, {"grid_cap": 1024},
-]
+SETTINGS = [{}] + [{"u_tile_bytes": tb, "u_unroll": u} for tb in (8192, 16384, 32768)
+                   for u in (1, 2, 4)] + [{"u_tile_bytes": 65536, "u_unroll": 1}]
 
 
 def main():
