@@ -518,11 +518,6 @@ int ghx_tune(const char* key, int32_t value)
                 throw invalid("u_tile_bytes must be a power of two in [1 KiB, 1 MiB]");
             g_tune.u_tile_bytes = uint32_t(value);
         }
-        else if (k == "u_unroll")
-        {
-            if (value != 1 && value != 2 && value != 4) throw invalid("u_unroll must be 1, 2 or 4");
-            g_tune.u_unroll = value;
-        }
         else if (k == "urun")
         {
             if (value < 0 || value > 1) throw invalid("urun must be 0 or 1");

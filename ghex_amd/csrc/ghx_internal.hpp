@@ -42,8 +42,6 @@ struct tuning
     uint32_t u_tile_bytes = 16384;     // tile of unstructured segments with long rows (config 5's
                                        // 64-B levels-first rows: scatter 16.8 -> 14.0 us against
                                        // 8 KiB, tools/u_tile_sweep.py, profiles/r05_u_tile_sweep*)
-    int u_unroll = 4;                  // vectors in flight per lane, unstructured general path
-                                       // (1, 2 or 4)
     int order = 1;                     // tile dispatch order: 0 segment order, 1 short-row
                                        // segments first (2-4 lost: tools/kernel_variants_r02.hip)
     int urun = 1;                      // unstructured 4/8-B-row segments: 16-B lane chunks with

@@ -808,22 +808,11 @@ int launch_put(const kargs& a, void* stream, uint32_t grid)
     return launched("put");
 }
 
-template<bool DBL, int UU>
-void launch_u_general(const kargs& a, int direction, hipStream_t s, uint32_t grid)
-{
-    if (direction == 0) launch((k_copy<true, seg_u, false, DBL, UU>), grid, s, a);
-    else launch((k_copy<false, seg_u, false, DBL, UU>), grid, s, a);
-}
-
 template<bool DBL>
 void launch_u_general(const kargs& a, int direction, hipStream_t s, uint32_t grid)
 {
-    switch (g_tune.u_unroll)
-    {
-        case 1: launch_u_general<DBL, 1>(a, direction, s, grid); break;
-        case 2: launch_u_general<DBL, 2>(a, direction, s, grid); break;
-        default: launch_u_general<DBL, 4>(a, direction, s, grid); break;
-    }
+    if (direction == 0) launch((k_copy<true, seg_u, false, DBL>), grid, s, a);
+    else launch((k_copy<false, seg_u, false, DBL>), grid, s, a);
 }
 
 int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid, bool runs)

@@ -52,8 +52,8 @@ typedef void* ghx_stream;
  * "xcd_pair" (0|1: line-sharing short-row segment pairs dispatched in lock-step groups of 8
  * tiles, same XCD), "short_pol" (field-side cache policy of short-row segments: bit 0
  * non-temporal loads, bit 1 sc1 stores), "u_tile_rows" (rows per tile of short-row index-list
- * segments), "urun" (0|1: run path for 4/8-B index-list rows), "u_run_tile_rows" (rows per tile
- * of run-heavy index lists), "self_tile_bytes" (tile of the fused self exchange),
+ * segments), "u_tile_bytes" (tile of index-list segments with long rows), "urun" (0|1: run path
+ * for 4/8-B index-list rows), "u_run_tile_rows" (rows per tile of run-heavy index lists), "self_tile_bytes" (tile of the fused self exchange),
  * "mixed_always" (0|1: build mixed self/peer plans even without short-row self messages);
  * "reset" restores every default. Plan-shaping knobs apply to plans created afterwards. Unknown
  * keys fail with GHX_ERR_INVALID (the variants removed in round 3 are listed in

@@ -380,3 +380,20 @@ def test_unstructured_more_buffers_than_one_launch_holds():
                     "outer": list(range(6, 6 + len(halo)))})
     run_unstructured({"nr": 2, "doms": out, "seed": 99,
                       "fields": [{"dtype": np.float64, "levels": 2, "first": True, "pad": 1}]})
+
+
+@pytest.mark.parametrize("knobs", [{"u_tile_bytes": 1024}, {"u_tile_bytes": 65536},
+                                   {"u_tile_rows": 3, "urun": 0},
+                                   {"small_row_bytes": 4096, "u_tile_rows": 5}])
+def test_unstructured_tuning_variants_stay_bit_exact(knobs):
+    """The unstructured general path (copy_tile_u: positions past a tile's end clamped to its
+    last vector) under tile sizes that leave partial and tiny tiles: the seeded random meshes
+    stay bit-exact."""
+    from ghex_amd import _ghx
+    try:
+        for k, v in knobs.items():
+            _ghx.call("ghx_tune", k.encode(), v)
+        for seed in range(12):
+            run_unstructured(draw_unstructured(seed))
+    finally:
+        _ghx.call("ghx_tune", b"reset", 0)

@@ -12,8 +12,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SETTINGS = [{}] + [{"u_tile_bytes": tb, "u_unroll": u} for tb in (8192, 16384, 32768)
-                   for u in (1, 2, 4)] + [{"u_tile_bytes": 65536, "u_unroll": 1}]
+# (round 5 also swept a per-lane unroll of 1/2/4 vectors, then removed: 4 was best at levels 8,
+# profiles/r05_u_tile_sweep.jsonl)
+SETTINGS = [{}] + [{"u_tile_bytes": tb} for tb in (8192, 16384, 32768, 65536)]
 
 
 def main():
