@@ -1039,6 +1039,11 @@ def _floor_lib():
     L.ghx_probe_fused_floor.restype = ctypes.c_int
     L.ghx_probe_fused_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_double)]
+    L.ghx_probe_multi_floor.restype = ctypes.c_int
+    L.ghx_probe_multi_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_int64)]
     P32 = ctypes.POINTER(ctypes.c_int32)
     L.ghx_probe_index_floor.restype = ctypes.c_int
     L.ghx_probe_index_floor.argtypes = [ctypes.c_int64, ctypes.c_int, P32, ctypes.c_int64, P32,
@@ -1076,6 +1081,36 @@ def index_floor(cells, levels, sends, recvs, k_gather, k_scatter):
                 if k_scatter else None,
                 "what": "the simplest gather / scatter kernels over the same lid lists (one fp64 "
                         "value per lane, no plan), kernel-own events, medians of 21"}
+    except Exception as e:  # reported, never fatal
+        return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+
+
+def multi_floor(N, H, elem_sizes, k_pack, k_unpack):
+    """Config 4's address-set floors (tools/pack_floor.hip ghx_probe_multi_floor): the fields
+    (element sizes `elem_sizes`) in one allocation at 2 MiB-aligned offsets. Pack: one 16-B load
+    per 128-B field line the pack reads (x-face lines first) + the buffer writes. Unpack: the
+    buffer read + every halo row's bytes written once (16/8/4-B pieces). Kernel-own events,
+    medians of 21, beside the product's pack / unpack launches (k_pack / k_unpack, seconds).
+    floor_over_kernel = probe time / product time (above 1: the product is faster)."""
+    import ctypes
+    try:
+        L = _floor_lib()
+        if L is None:
+            return {"error": "tools/lib/libpackfloor.so not built (make -C tools)"}
+        us = (ctypes.c_double * 4)()
+        c = (ctypes.c_int64 * 3)()
+        es = (ctypes.c_int * len(elem_sizes))(*elem_sizes)
+        rc = L.ghx_probe_multi_floor(N, H, len(elem_sizes), es, 21, us, c)
+        if rc:
+            return {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
+        return {"lines": c[0], "pieces": c[1], "halo_bytes": c[2],
+                "pack_floor_us": round(us[0], 2), "pack_floor_cold_us": round(us[1], 2),
+                "unpack_floor_us": round(us[2], 2), "unpack_floor_cold_us": round(us[3], 2),
+                "pack_kernel_us": round(k_pack * 1e6, 2),
+                "unpack_kernel_us": round(k_unpack * 1e6, 2),
+                "pack_floor_over_kernel": round(us[0] / (k_pack * 1e6), 3) if k_pack else None,
+                "unpack_floor_over_kernel": round(us[2] / (k_unpack * 1e6), 3)
+                if k_unpack else None}
     except Exception as e:  # reported, never fatal
         return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
 
@@ -1618,6 +1653,13 @@ def bench_config4(torch, dev, ghex_amd, R, cpu_seconds=None):
     torch.cuda.synchronize(dev)
     ok = all_ok()
     del keep
+
+    def pk(s):
+        _ghx.check(L.ghx_exchange_pack(plan.h, fptr, 5, sptr, len(send), s), "pack")
+
+    def up(s):
+        _ghx.check(L.ghx_exchange_unpack(plan.h, fptr, 5, sptr, len(send), s), "unpack")
+    kp, ku = launch_durations(torch, dev, torch.cuda.current_stream(dev), _ghx, [pk, up])
     n = E ** 3 - N ** 3
     nbytes = 4 * n * (3 * 8 + 2 * 4)
     out = {"GBps": round(nbytes / t2 / 1e9, 1), "frac": round(nbytes / t2 / 1e9 / HBM_PEAK_GBS, 4),
@@ -1630,7 +1672,8 @@ def bench_config4(torch, dev, ghex_amd, R, cpu_seconds=None):
            "verified_fused": ok_fused,
            "verified_fused_what": "the first co.exchange() (the fused k_self launch)",
            "fused_self": {"us_per_exchange": round(t * 1e6, 2),
-                          "bytes_moved": 3 * n * (3 * 8 + 2 * 4)} if fusedp else None}
+                          "bytes_moved": 3 * n * (3 * 8 + 2 * 4)} if fusedp else None,
+           "floor": multi_floor(N, H, [8 if t == "f64" else 4 for t in CONFIG4_TYPES], kp, ku)}
     if cpu_seconds:
         gpu_buf = send[0][:plan.send[0]["size"]].cpu().numpy()
         out["cpu_baseline"] = cpu_baseline_config4(cpu_seconds, gpu_buf)

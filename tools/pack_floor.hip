@@ -474,6 +474,182 @@ done:
     return rc;
 }
 
+
+
+// Config 4's floors (round 5): several fields of element sizes es[k] (one (N+2H)^3 periodic
+// domain each, layout_map<2,1,0>), placed in one allocation at 2 MiB-aligned offsets. Pack:
+// one 16-B load per 128-B line the pack must read (x-face lines of every field first, as the
+// plan dispatches short-row segments first), then the buffer writes (every field's halo bytes).
+// Unpack: the buffer read, then every halo row's bytes written once in 16/8/4-B pieces
+// (encoding: byte address / 4 in bits 0-29, size code in bits 30-31: 0 = 4 B, 1 = 8 B, 2 = 16 B).
+static void field_lines(int N, int H, int es, uint64_t base, std::vector<uint8_t>& cls, uint64_t& useful)
+{
+    const int E = N + 2 * H;
+    const uint64_t pitch = uint64_t(E) * es, plane = pitch * E;
+    const int lo[3] = {H, H, N};
+    const int hi[3] = {2 * H - 1, N + H - 1, N + H - 1};
+    for (int dz = 0; dz < 3; ++dz)
+        for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx)
+            {
+                if (dx == 1 && dy == 1 && dz == 1) continue;
+                const int x0 = lo[dx], x1 = hi[dx];
+                const bool shortrow = uint64_t(x1 - x0 + 1) * es < 64;
+                for (int z = lo[dz]; z <= hi[dz]; ++z)
+                    for (int y = lo[dy]; y <= hi[dy]; ++y)
+                    {
+                        const uint64_t b = base + uint64_t(z) * plane + uint64_t(y) * pitch + uint64_t(x0) * es;
+                        const uint64_t e = b + uint64_t(x1 - x0 + 1) * es;
+                        useful += e - b;
+                        for (uint64_t l = b / 128; l <= (e - 1) / 128; ++l)
+                            if (shortrow) cls[l] = 1;
+                            else if (!cls[l]) cls[l] = 2;
+                    }
+            }
+}
+
+static void field_pieces(int N, int H, int es, uint64_t base, std::vector<uint32_t>& xf,
+                         std::vector<uint32_t>& lg)
+{
+    const int E = N + 2 * H;
+    const uint64_t pitch = uint64_t(E) * es, plane = pitch * E;
+    const int lo[3] = {0, H, N + H};
+    const int hi[3] = {H - 1, N + H - 1, N + 2 * H - 1};
+    for (int dz = 0; dz < 3; ++dz)
+        for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx)
+            {
+                if (dx == 1 && dy == 1 && dz == 1) continue;
+                const int x0 = lo[dx], x1 = hi[dx];
+                auto& out = uint64_t(x1 - x0 + 1) * es < 64 ? xf : lg;
+                for (int z = lo[dz]; z <= hi[dz]; ++z)
+                    for (int y = lo[dy]; y <= hi[dy]; ++y)
+                    {
+                        uint64_t b = base + uint64_t(z) * plane + uint64_t(y) * pitch + uint64_t(x0) * es;
+                        const uint64_t e = b + uint64_t(x1 - x0 + 1) * es;
+                        while (b < e)
+                        {
+                            uint32_t code = 0, w = 4;
+                            if (b % 16 == 0 && e - b >= 16) code = 2, w = 16;
+                            else if (b % 8 == 0 && e - b >= 8) code = 1, w = 8;
+                            out.push_back(uint32_t(b / 4) | (code << 30));
+                            b += w;
+                        }
+                    }
+            }
+}
+
+__global__ __launch_bounds__(256) void k_pieces4(const uint32_t* __restrict__ pieces, uint32_t n,
+                                                 char* __restrict__ field, const v4* __restrict__ buf,
+                                                 uint64_t rvec, unsigned* sink)
+{
+    v4 acc{0, 0, 0, 0};
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < rvec; i += uint64_t(stride)) acc ^= buf[i];
+    for (uint32_t base = blockIdx.x * 256u + threadIdx.x; base < n; base += kU * stride)
+    {
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+        {
+            if (base + u * stride >= n) break;
+            const uint32_t q = pieces[base + u * stride];
+            char* a = field + uint64_t(q & 0x3fffffffu) * 4;
+            const uint32_t code = q >> 30;
+            if (code == 2) *(v4*)a = v4{q, acc.x, 2, 3};
+            else if (code == 1) *(unsigned __attribute__((ext_vector_type(2)))*)a = {q, acc.y};
+            else *(unsigned*)a = q ^ acc.z;
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
+}
+
+// out_us[4]: {pack floor warm, cold, unpack floor warm, cold}; counts[3]: lines, pieces, useful
+// bytes. Returns 0, or the failing source line.
+extern "C" int ghx_probe_multi_floor(int N, int H, int n_fields, const int* es, int reps,
+                                     double* out_us, int64_t* counts)
+{
+    int rc = 0;
+    const int E = N + 2 * H;
+    std::vector<uint64_t> base(static_cast<size_t>(n_fields));
+    uint64_t total = 0;
+    for (int k = 0; k < n_fields; ++k)
+    {
+        base[size_t(k)] = total;
+        total += (uint64_t(E) * E * E * es[k] + (uint64_t(2) << 20) - 1) / (uint64_t(2) << 20) * (uint64_t(2) << 20);
+    }
+    std::vector<uint8_t> cls(size_t(total / 128 + 1), 0);
+    uint64_t useful = 0;
+    for (int k = 0; k < n_fields; ++k) field_lines(N, H, es[k], base[size_t(k)], cls, useful);
+    std::vector<uint32_t> lines;
+    for (int pass = 1; pass <= 2; ++pass)
+        for (size_t l = 0; l < cls.size(); ++l)
+            if (cls[l] == pass) lines.push_back(uint32_t(l));
+    std::vector<uint32_t> pxf, plg;
+    for (int k = 0; k < n_fields; ++k) field_pieces(N, H, es[k], base[size_t(k)], pxf, plg);
+    std::vector<uint32_t> pieces(pxf);
+    pieces.insert(pieces.end(), plg.begin(), plg.end());
+    counts[0] = int64_t(lines.size());
+    counts[1] = int64_t(pieces.size());
+    counts[2] = int64_t(useful);
+    const size_t flush_bytes = size_t(1) << 30;
+    char *field = nullptr, *fl = nullptr;
+    v4* buf = nullptr;
+    unsigned* sink = nullptr;
+    uint32_t *d_l = nullptr, *d_p = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const int grid = 256 * 8;
+    if (total / 4 >= (uint64_t(1) << 30)) return __LINE__;
+    CK(hipMalloc(&field, total));
+    CK(hipMalloc(&fl, flush_bytes));
+    CK(hipMalloc(&buf, useful + 64));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMalloc(&d_l, lines.size() * 4 + 4));
+    CK(hipMalloc(&d_p, pieces.size() * 4 + 4));
+    CK(hipMemcpy(d_l, lines.data(), lines.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_p, pieces.data(), pieces.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(field, 1, total));
+    CK(hipMemset(buf, 3, useful + 64));
+    CK(hipMemset(fl, 2, flush_bytes));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int j = 0; j < 2; ++j)
+        for (int cold = 0; cold < 2; ++cold)
+        {
+            auto go = [&](hipEvent_t a, hipEvent_t b) {
+                if (j == 0)
+                    hipExtLaunchKernelGGL(k_lines, dim3(grid), dim3(256), 0, 0, a, b, 0, d_l,
+                                          uint32_t(lines.size()), (const char*)field, buf,
+                                          uint64_t(useful / 16), sink);
+                else
+                    hipExtLaunchKernelGGL(k_pieces4, dim3(grid), dim3(256), 0, 0, a, b, 0, d_p,
+                                          uint32_t(pieces.size()), field, (const v4*)buf,
+                                          uint64_t(useful / 16), sink);
+            };
+            std::vector<float> t;
+            for (int i = 0; i < reps; ++i)
+            {
+                if (cold)
+                    hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, 0, (const v4*)fl,
+                                       flush_bytes / 16, sink);
+                else
+                    go(nullptr, nullptr);
+                go(e0, e1);
+                CK(hipEventSynchronize(e1));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                t.push_back(ms * 1e3f);
+            }
+            std::sort(t.begin(), t.end());
+            out_us[2 * j + cold] = t[t.size() / 2];
+        }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    for (void* p : {(void*)field, (void*)fl, (void*)buf, (void*)sink, (void*)d_l, (void*)d_p})
+        if (p) (void)hipFree(p);
+    return rc;
+}
+
 #ifdef PACK_FLOOR_MAIN
 int main(int argc, char** argv)
 {
