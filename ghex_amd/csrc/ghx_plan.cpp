@@ -99,16 +99,20 @@ template<typename Seg>
 std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
 {
     std::vector<std::vector<uint32_t>> per(segs.size());
-    uint64_t short_rows = 0;  // the plan's short rows (one launch's request-bound work)
+    // each field's short rows (its request-bound work): a field's short-row tiles are sized by
+    // its own rows, not the plan's, so a plan of several fields keeps each field's tiling
+    // (config 4, five 256^3 fields at H=3: 2048-row tiles by the plan's 686k short rows vs 512
+    // by each field's 137k, pack 23.7 -> 21.4 us, profiles/r05_config4_sweep.jsonl)
+    std::map<int32_t, uint64_t> short_rows;
     for (const auto& sg : segs)
-        if (sg.row_bytes < g_tune.small_row_bytes) short_rows += sg.bytes / sg.row_bytes;
+        if (sg.row_bytes < g_tune.small_row_bytes) short_rows[sg.field_slot] += sg.bytes / sg.row_bytes;
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
         const bool small = segs[i].row_bytes < g_tune.small_row_bytes;
         uint32_t tb = long_tile_bytes(segs[i]);
         if (small)
         {
-            const uint32_t rows = short_tile_rows(segs[i], short_rows);
+            const uint32_t rows = short_tile_rows(segs[i], short_rows[segs[i].field_slot]);
             const uint64_t want = uint64_t(rows) * segs[i].row_bytes;
             tb = uint32_t(std::max<uint64_t>(segs[i].row_bytes, std::min<uint64_t>(want, kMaxTileBytes)));
             tb -= tb % segs[i].row_bytes;  // whole rows per tile
