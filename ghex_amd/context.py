@@ -224,6 +224,11 @@ class LoopbackWorld:
     def run(self, fn):
         import threading
         res, err = [None] * self.n, []
+        # a fresh rendezvous per run: an earlier run's failure leaves its barrier broken and
+        # possibly undelivered mail
+        self._bar = threading.Barrier(self.n)
+        self._slots = [None] * self.n
+        self._mail = {}
 
         def body(r):
             try:

@@ -484,3 +484,25 @@ def test_unstructured_pattern_edge_cases():
                 got = [(rr, tag, rid, lids) for rid, rr, tag, lids in pc.halos(0, direction)]
                 exp = [(rr, tag, rid, lids) for (rr, tag), (rid, lids) in opats[r][0][key].items()]
                 assert got == exp, (hgs, r, key)
+
+
+def test_loopback_world_reusable_after_failure():
+    """A rank that raises aborts the run (the others leave their barrier) and its error is
+    re-raised; the same LoopbackWorld then runs again with a fresh rendezvous."""
+    from ghex_amd.context import LoopbackWorld
+    w = LoopbackWorld(3)
+
+    def bad(ctx):
+        if ctx.rank() == 1:
+            raise ValueError("rank 1 failed")
+        return ctx.all_gather_object(ctx.rank())
+
+    with pytest.raises(ValueError, match="rank 1 failed"):
+        w.run(bad)
+
+    def good(ctx):
+        got = ctx.exchange_arrays([((ctx.rank() + 1) % 3, [ctx.rank()] * 2)],
+                                  [((ctx.rank() - 1) % 3, 2)])
+        return ctx.all_gather_object(ctx.rank()), [int(x) for x in got[0]]
+
+    assert w.run(good) == [([0, 1, 2], [2, 2]), ([0, 1, 2], [0, 0]), ([0, 1, 2], [1, 1])]
