@@ -1010,17 +1010,30 @@ def extras(args, torch, dist, dev, stream, out, v):
         torch.cuda.empty_cache()
         cs = None if (rank != 0 or args.no_cpu_baseline) else args.cpu_config_seconds
         ex = out["extra_configs"] = {}
-        ex["config4_5fields_256^3_h3_f64f32"] = bench_config4(torch, dev, ghex_amd, R, cs)
-        pats, t_all, t_rank = config5_patterns()
-        for lv in (1, 8):
-            ex[f"config5_unstructured_10M_5pct_levels{lv}"] = bench_config5(
-                torch, dev, _ghx, lv, pats, cs)
-        ex["config5_pattern_setup"] = {
-            "ranks": 8, "cells_per_rank": int(pats[0][0].size - pats[0][1].size),
-            "seconds_all_ranks": round(t_all, 2), "seconds_max_rank": round(t_rank, 2),
-            "what": "8 ranks as threads of this process (LoopbackWorld), each generating its "
-                    "domain and running the product make_pattern<unstructured> (reduced halos)"}
-        del pats
+        # each config reported on its own: a failure is recorded in its entry and the ones after
+        # it (and the headline's cpu_baseline) still run
+        try:
+            ex["config4_5fields_256^3_h3_f64f32"] = bench_config4(torch, dev, ghex_amd, R, cs)
+        except Exception as e:
+            ex["config4_5fields_256^3_h3_f64f32"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+        torch.cuda.empty_cache()
+        try:
+            pats, t_all, t_rank = config5_patterns()
+            for lv in (1, 8):
+                name = f"config5_unstructured_10M_5pct_levels{lv}"
+                try:
+                    ex[name] = bench_config5(torch, dev, _ghx, lv, pats, cs)
+                except Exception as e:
+                    ex[name] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+                torch.cuda.empty_cache()
+            ex["config5_pattern_setup"] = {
+                "ranks": 8, "cells_per_rank": int(pats[0][0].size - pats[0][1].size),
+                "seconds_all_ranks": round(t_all, 2), "seconds_max_rank": round(t_rank, 2),
+                "what": "8 ranks as threads of this process (LoopbackWorld), each generating its "
+                        "domain and running the product make_pattern<unstructured> (reduced halos)"}
+            del pats
+        except Exception as e:
+            ex["config5_pattern_setup"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, Hw, args.cpu_seconds)
 
