@@ -11,6 +11,7 @@ from typing import Sequence
 from .. import _ghx
 from ..communication_object import CommunicationObject
 from ..pattern import PatternContainer
+from .cartesian_sets import IndexSpace, ProductSet, UnitRange, union  # noqa: F401 (re-exported)
 
 
 def make_communication_object(context, **options) -> CommunicationObject:
@@ -21,61 +22,10 @@ def _corners(index_set):
     """(first, last) of a box given as the reference binding's index sets do it
     (bindings/python/src/ghex/structured/regular.py:31-38, 111-135): any object with `ndim` and
     corner indexing, set[(0,)*ndim] = first cell, set[(-1,)*ndim] = last cell (e.g. a
-    cartesian_sets.ProductSet, or ghex_amd.structured.ProductSet)."""
+    cartesian_sets.ProductSet or ghex_amd.structured.cartesian_sets.ProductSet)."""
     nd = int(index_set.ndim)
     return (tuple(int(x) for x in index_set[(0,) * nd]),
             tuple(int(x) for x in index_set[(-1,) * nd]))
-
-
-class UnitRange:
-    """Integers start <= i < stop (the index-set vocabulary of the reference Python binding,
-    bindings/python/src/ghex/structured/cartesian_sets.py)."""
-
-    def __init__(self, start: int, stop: int):
-        self.start, self.stop = int(start), int(stop)
-        if self.stop < self.start:
-            raise ValueError("UnitRange: stop < start")
-
-    def __len__(self):
-        return self.stop - self.start
-
-    def __getitem__(self, i: int) -> int:
-        n = len(self)
-        if not -n <= i < n:
-            raise IndexError(i)
-        return self.start + (i % n)
-
-    def __mul__(self, other):
-        """rx * ry * rz: the product box (cartesian_sets.py's UnitRange.__mul__)."""
-        return ProductSet(self) * other
-
-
-class ProductSet:
-    """The Cartesian product of UnitRanges: a box of cells, indexable by corner tuples."""
-
-    def __init__(self, *ranges: UnitRange):
-        self.ranges = tuple(ranges)
-
-    @classmethod
-    def from_coords(cls, first: Sequence[int], last: Sequence[int]) -> "ProductSet":
-        return cls(*(UnitRange(f, l + 1) for f, l in zip(first, last)))
-
-    @property
-    def ndim(self) -> int:
-        return len(self.ranges)
-
-    @property
-    def shape(self):
-        return tuple(len(r) for r in self.ranges)
-
-    def __getitem__(self, idx):
-        if len(idx) != self.ndim:
-            raise IndexError(idx)
-        return tuple(r[i] for r, i in zip(self.ranges, idx))
-
-    def __mul__(self, other):
-        more = other.ranges if isinstance(other, ProductSet) else (other,)
-        return ProductSet(*self.ranges, *more)
 
 
 class DomainDescriptor:
@@ -152,22 +102,32 @@ class HaloGenerator:
         loc = (_ghx.Box * max(1, n.value))()
         glo = (_ghx.Box * max(1, n.value))()
         _ghx.call("ghx_regular_halo_boxes", *args, loc, glo, n.value, ctypes.byref(n))
-        return HaloBoxes((tuple(loc[i].first[:D]), tuple(loc[i].last[:D]),
-                          tuple(glo[i].first[:D]), tuple(glo[i].last[:D])) for i in range(n.value))
+        boxes = HaloBoxes((tuple(loc[i].first[:D]), tuple(loc[i].last[:D]),
+                           tuple(glo[i].first[:D]), tuple(glo[i].last[:D])) for i in range(n.value))
+        boxes.ndim = D
+        return boxes
 
 
 class HaloBoxes(list):
     """The receive boxes of a domain, [(local_first, local_last, global_first, global_last)] in
-    generation order; `.local` / `.global_` give them as ProductSets, the two halves of the
-    reference binding's HaloContainer (bindings/python/src/ghex/structured/regular.py:105-154)."""
+    generation order; `.local` / `.global_` are the two halves of the reference binding's
+    HaloContainer (bindings/python/src/ghex/structured/regular.py:105-154): each the union of
+    the boxes as one index set (cartesian_sets.union, simplified like the reference's)."""
+
+    ndim = 3
+
+    def _set(self, lo, hi):
+        if not self:
+            return ProductSet(*([UnitRange(0, 0)] * self.ndim))
+        return union(*(ProductSet.from_coords(b[lo], b[hi]) for b in self))
 
     @property
     def local(self):
-        return [ProductSet.from_coords(b[0], b[1]) for b in self]
+        return self._set(0, 1)
 
     @property
     def global_(self):
-        return [ProductSet.from_coords(b[2], b[3]) for b in self]
+        return self._set(2, 3)
 
 
 def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[DomainDescriptor]):

@@ -1,0 +1,106 @@
+"""The reference binding's structured pattern test (test/bindings/python/test_structured_pattern.py)
+run against ghex_amd with its own vocabulary (cartesian_sets.IndexSpace, DomainDescriptor,
+HaloGenerator, make_pattern, make_field_descriptor, make_communication_object), the MPI ranks
+emulated in one process on one GPU (tests/gpu_util.py: FakeContext + an in-process router for the
+peer messages). Fields are device tensors in the reference's order="F" layout. Besides the
+reference's own check (interior-index halo cells hold their owner's coordinates and rank), the
+periodic halo cells are checked too, their owner found by wrapping the global index."""
+import pytest
+
+from tests.test_cartesian_sets import cart_coords, compute_dims
+
+pytestmark = pytest.mark.gpu
+
+SIZES = (48, 24, 16)
+HALOS_PER_DIM = ((2, 1), (1, 2), (1, 1))
+
+
+def _f_order_zeros(torch, shape):
+    """np.zeros(shape, order="F") as a device tensor: dimension 0 fastest in memory."""
+    return torch.zeros(tuple(reversed(shape)), dtype=torch.float64,
+                       device="cuda").permute(*reversed(range(len(shape))))
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("periodic", [True, False])
+@pytest.mark.parametrize("ndim", [1, 2, 3])
+def test_pattern(ndim, periodic, world):
+    import torch
+    from ghex_amd.structured.cartesian_sets import IndexSpace
+    from ghex_amd.structured.regular import (DomainDescriptor, HaloGenerator,
+                                             make_communication_object, make_field_descriptor,
+                                             make_pattern)
+    from tests.gpu_util import FakeContext, emulated_exchange
+
+    dims = compute_dims(world, ndim)
+    halos = tuple(HALOS_PER_DIM[d] for d in range(ndim))
+    periodicity = tuple(periodic if d == 0 else True for d in range(ndim))
+    global_grid = IndexSpace.from_sizes(*SIZES[:ndim])
+    sub_grids = global_grid.decompose(dims)
+    halo_gen = HaloGenerator(global_grid.subset["definition"], halos, periodicity)
+
+    ranks = []
+    for r in range(world):
+        p_coord = cart_coords(r, dims)
+        owned = sub_grids[p_coord].subset["definition"]
+        sub_grid = IndexSpace({"definition": owned,
+                               "halo": owned.extend(*halos).without(owned)})
+        memory_local_grid = sub_grid.translate(*(-o for o in sub_grid.bounds[(0,) * ndim]))
+        ranks.append(dict(coord=p_coord, owned=owned, sub_grid=sub_grid,
+                          mem=memory_local_grid, dd=DomainDescriptor(r, owned)))
+    table = {r: [(r, x["dd"].first(), x["dd"].last())] for r, x in enumerate(ranks)}
+    cos, pats = [], []
+    for r, x in enumerate(ranks):
+        ctx = FakeContext(r, world, table)
+        pats.append(make_pattern(ctx, halo_gen, [x["dd"]]))
+        cos.append(make_communication_object(ctx))
+
+    def make_field(x):
+        f = _f_order_zeros(torch, x["mem"].bounds.shape)
+        return f, make_field_descriptor(x["dd"], f, x["mem"].subset["definition"][(0,) * ndim],
+                                        x["mem"].bounds.shape)
+
+    fields, gfields, rank_fields, grank_fields = [], [], [], []
+    for r, x in enumerate(ranks):
+        fs, gs = zip(*(make_field(x) for _ in range(ndim)))
+        for d, c in enumerate(x["coord"]):
+            fs[d][...] = c
+        fields.append(fs)
+        gfields.append(gs)
+        rf, grf = make_field(x)
+        rf[...] = r
+        rank_fields.append(rf)
+        grank_fields.append(grf)
+    emulated_exchange(cos, [[pats[r](g) for g in gfields[r]] for r in range(world)])
+    emulated_exchange(cos, [[pats[r](grank_fields[r])] for r in range(world)])
+
+    last = global_grid.subset["definition"][(-1,) * ndim]
+    size = SIZES[:ndim]
+    checked = wrapped = 0
+    for r, x in enumerate(ranks):
+        fh = [f.cpu().numpy() for f in fields[r]]
+        rh = rank_fields[r].cpu().numpy()
+        for m_idx, local_idx in zip(x["mem"].bounds, x["sub_grid"].bounds):
+            owner_coord = tuple(int(fh[d][m_idx]) for d in range(ndim))
+            inside = all(0 <= l <= last[d] for d, l in enumerate(local_idx))
+            if inside:  # the reference's check
+                assert local_idx in sub_grids[owner_coord].subset["definition"], (r, local_idx)
+                assert rh[m_idx] == dims_rank(owner_coord, dims), (r, local_idx)
+                checked += 1
+            elif all(periodicity[d] or 0 <= l <= last[d] for d, l in enumerate(local_idx)):
+                g = tuple(l % size[d] for d, l in enumerate(local_idx))
+                if local_idx in x["sub_grid"].subset["halo"]:
+                    assert g in sub_grids[owner_coord].subset["definition"], (r, local_idx)
+                    assert rh[m_idx] == dims_rank(owner_coord, dims), (r, local_idx)
+                    wrapped += 1
+    assert checked > 0
+    if any(periodicity):
+        assert wrapped > 0
+
+
+def dims_rank(coord, dims):
+    """MPI_Cart_rank (row-major)."""
+    r = 0
+    for c, d in zip(coord, dims):
+        r = r * d + c
+    return r

@@ -165,9 +165,11 @@ def test_reference_binding_index_set_signatures():
     assert a.halos == b.halos and a.periodic == b.periodic
     assert a(dd) == b(DomainDescriptor(7, (3, 0, 2), (8, 4, 3))) and len(a(dd)) > 0
     boxes = a(dd)
-    assert [(g.ranges[0].start, g[(-1, -1, -1)]) for g in boxes.global_] == \
-        [(gf[0], gl) for (_, _, gf, gl) in boxes]
-    assert [l.shape for l in boxes.local] == [g.shape for g in boxes.global_]
+    # .global_ / .local: the boxes' union as one index set (the reference's HaloContainer)
+    from ghex_amd.structured.cartesian_sets import union
+    assert boxes.global_ == union(*(ProductSet.from_coords(gf, gl) for (_, _, gf, gl) in boxes))
+    assert boxes.local.size == boxes.global_.size == sum(
+        ProductSet.from_coords(lf, ll).size for (lf, ll, _, _) in boxes)
     with pytest.raises(IndexError):
         UnitRange(0, 2)[2]
     with pytest.raises(ValueError):
