@@ -1,4 +1,5 @@
 """The reference binding's structured pattern test (test/bindings/python/test_structured_pattern.py)
+and unstructured domain test (test_unstructured_domain_descriptor.py::test_domain_descriptor)
 run against ghex_amd with its own vocabulary (cartesian_sets.IndexSpace, DomainDescriptor,
 HaloGenerator, make_pattern, make_field_descriptor, make_communication_object), the MPI ranks
 emulated in one process on one GPU (tests/gpu_util.py: FakeContext + an in-process router for the
@@ -104,3 +105,69 @@ def dims_rank(coord, dims):
     for c, d in zip(coord, dims):
         r = r * d + c
     return r
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32", "int32", "int64"])
+def test_unstructured_domain_descriptor(golden_dir, dtype):
+    """test/bindings/python/test_unstructured_domain_descriptor.py::test_domain_descriptor on 4
+    emulated ranks (its fixture: tests/golden/unstructured_case.json "python_fixture"): each rank
+    one domain with HaloGenerator.from_gids(outer), two fields of LEVELS=2 (order "C": levels
+    first; order "F": levels as the outer stride) in one exchange; inner cells hold
+    rank*1000 + 10*gid + level, halos -1 before; afterwards every halo value's last three digits
+    are 10*gid + level, as the reference checks."""
+    import json
+    import os
+
+    import numpy as np
+    import torch
+    from ghex_amd import unstructured as U
+    from ghex_amd.context import LoopbackWorld
+    from tests.gpu_util import FakeContext, emulated_exchange
+
+    with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
+        fx = json.load(fh)["python_fixture"]
+    L, doms = fx["levels"], fx["domains"]
+    W = 4
+
+    def rank_fn(ctx):
+        d = doms[str(ctx.rank())]
+        dd = U.DomainDescriptor(ctx.rank(), d["all"], d["outer_lids"])
+        return dd, U.make_pattern(ctx, U.HaloGenerator.from_gids(d["outer"]), [dd])
+
+    pats = LoopbackWorld(W).run(rank_fn)
+    table = {r: [] for r in range(W)}
+    cos, bis, fields = [], [], []
+    for r in range(W):
+        d = doms[str(r)]
+        dd, pattern = pats[r]
+        assert dd.domain_id() == r
+        assert dd.size() == len(d["all"])
+        assert dd.inner_size() == len(d["inner"])
+        inner = set(d["inner"])
+        host = np.array([[r * 1000 + 10 * g + l if g in inner else -1 for l in range(L)]
+                         for g in d["all"]], dtype=dtype)
+        mine = []
+        bis.append([])
+        for order in ("C", "F"):
+            a = np.array(host, order=order)
+            t = torch.from_numpy(a).cuda() if order == "C" else \
+                torch.from_numpy(np.ascontiguousarray(a.T)).cuda().t()
+            fd = U.make_field_descriptor(dd, t)
+            assert fd.levels_first == (order == "C")
+            mine.append((order, t))
+            bis[r].append(pattern(fd))
+        fields.append(mine)
+        cos.append(U.make_communication_object(FakeContext(r, W, table)))
+    emulated_exchange(cos, bis)
+    for r in range(W):
+        d = doms[str(r)]
+        inner = set(d["inner"])
+        for order, t in fields[r]:
+            got = t.cpu().numpy()
+            for x, g in enumerate(d["all"]):
+                for l in range(L):
+                    if g in inner:
+                        assert got[x, l] == r * 1000 + 10 * g + l, (r, order, x)
+                    else:
+                        v = int(got[x, l])
+                        assert v - 1000 * int(v / 1000) == 10 * g + l, (r, order, x, v)
