@@ -13,6 +13,22 @@ from .bulk_communication_object import (BulkCommunicationObject,  # noqa: F401
 
 __version__ = "0.1.0"
 
+# the build configuration, as the reference's ghex.__config__ / config() / print_config()
+# (bindings/python/src/_pyghex/config.cpp): the exchange's transport is torch.distributed
+# ("nccl" = RCCL between GPUs, gloo for host staging), the kernels are gfx950 HIP.
+__config__ = {"transport": "RCCL", "gpu": True, "gpu_mode": "hip", "xpmem": False,
+              "version": __version__, "arch": "gfx950"}
+
+
+def config() -> dict:
+    return dict(__config__)
+
+
+def print_config(d: dict = None) -> None:
+    d = config() if d is None else d
+    print("GHEX's configuration:\n" + "".join(f"     {k:<16}: {str(v):>10}\n" for k, v in d.items()),
+          end="")
+
 
 def native_library():
     """Load (and return) libghx.so; raises ImportError if it has not been built."""

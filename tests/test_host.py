@@ -506,3 +506,17 @@ def test_loopback_world_reusable_after_failure():
         return ctx.all_gather_object(ctx.rank()), [int(x) for x in got[0]]
 
     assert w.run(good) == [([0, 1, 2], [2, 2]), ([0, 1, 2], [0, 0]), ([0, 1, 2], [1, 1])]
+
+
+@pytest.mark.parametrize("thread_safe", [True, False])
+def test_context_and_config_like_the_reference(thread_safe, capsys):
+    """test/bindings/python/test_context.py: the module's version and configuration, and a
+    context over one process (here: no torch.distributed group = the single rank)."""
+    import ghex_amd
+    from ghex_amd.context import make_context
+    assert ghex_amd.__version__ and ghex_amd.__config__["gpu"] is True
+    assert ghex_amd.config() == ghex_amd.__config__ and ghex_amd.config() is not ghex_amd.__config__
+    ghex_amd.print_config()
+    assert "transport" in capsys.readouterr().out
+    ctx = make_context(None, thread_safe)
+    assert ctx.size() == 1 and ctx.rank() == 0
