@@ -57,10 +57,15 @@ def test_bench_line_n1_small():
     c4 = ex["config4_5fields_256^3_h3_f64f32"]
     assert c4["verified"] is True and c4["verified_fused"] is True and "timed hipGraph" in \
         c4["verified_what"]
+    fl = c4["floor"]  # the five-field floor probe beside the two launches
+    assert "error" not in fl, fl
+    assert fl["pack_floor_over_kernel"] > 0 and fl["unpack_floor_over_kernel"] > 0
+    assert fl["halo_bytes"] * 4 == c4["bytes_per_exchange"]
     for lv in (1, 8):
         c5 = ex[f"config5_unstructured_10M_5pct_levels{lv}"]
         assert c5["verified"] is True and c5["halo_cells"] == 500_000 and c5["peers"] == 7, c5
         assert "cpu_baseline" not in c5  # --no-cpu-baseline
+        assert "error" not in c5["index_floor"] and c5["index_floor"]["gather_us"] > 0, c5
     assert ex["config5_pattern_setup"]["ranks"] == 8
 
 
