@@ -98,6 +98,10 @@ def parse():
     return p.parse_args()
 
 
+# the one JSON line: whether rank 0 printed it, and the guard that can print a null one
+_LINE = {"guard": None, "printed": False}
+
+
 class StageGuard:
     """Bounds the stages before the headline line can be printed (init_process_group, the first
     cross-GPU exchange, the timed region). If a stage does not finish in time — a peer died or
@@ -125,6 +129,16 @@ class StageGuard:
         sys.stderr.flush()
         os._exit(self.EXIT_CODE)
 
+    def fail(self, name, exc):
+        """A stage raised: rank 0 prints the line with value null and the error (the exception
+        then propagates, so the process still fails)."""
+        o = dict(self.line)
+        o.update(value=None, verified=False, stage=name,
+                 error=f"stage '{name}' failed on rank {self.rank}: "
+                       f"{type(exc).__name__}: {str(exc)[:300]}; no measurement")
+        print(json.dumps(o), file=sys.stdout if self.rank == 0 else sys.stderr, flush=True)
+        _LINE["printed"] = True
+
     def stage(self, name, seconds):
         import contextlib
         import threading
@@ -139,6 +153,10 @@ class StageGuard:
             threading.Thread(target=watch, daemon=True, name=f"guard:{name}").start()
             try:
                 yield
+            except Exception as e:
+                done.set()
+                self.fail(name, e)
+                raise
             finally:
                 done.set()
         return guarded()
@@ -461,6 +479,7 @@ def main():
         "metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "config": {"N": N, "halo": Hw, "decomposition": list(parts)}}, rank)
+    _LINE["guard"] = guard
     with guard.stage("init_process_group", args.init_timeout):
         if distributed:
             import datetime
@@ -739,6 +758,7 @@ def main():
     def emit(o):
         if rank == 0 and printed.acquire(blocking=False):
             print(json.dumps(o), flush=True)
+            _LINE["printed"] = True
 
     extras_done = threading.Event()
 
@@ -2135,4 +2155,9 @@ def cpu_baseline_config5(seconds, host, sends, recvs, peer_bytes, gpu_sbufs, lev
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:  # a line with value null and the error, then the failure itself
+        if _LINE["guard"] is not None and not _LINE["printed"]:
+            _LINE["guard"].fail("main", e)
+        raise

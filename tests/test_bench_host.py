@@ -20,7 +20,30 @@ def test_spawned_ranks_fail_fast_without_a_gpu():
                         "--steps", "1", "--warmup", "0", "--N", "8"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert p.returncode != 0
-    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+    # no measurement: at most rank 0's line with value null and the failing stage's error
+    import json
+    for l in [l for l in p.stdout.splitlines() if l.startswith("{")]:
+        d = json.loads(l)
+        assert d["value"] is None and d["verified"] is False and "failed" in d["error"], d
+
+
+def test_a_failing_stage_prints_a_null_line():
+    """Single rank without a GPU: the first stage raises; the line still comes out (value null,
+    the stage and its error) and the process fails."""
+    import json
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("this checks the failure path; a GPU would run the bench")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1",
+                        "--warmup", "0", "--no-extras"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode != 0
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["stage"] == "init_process_group" and "HIP" in d["error"]
 
 
 def test_world_size_mismatch_is_refused():
