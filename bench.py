@@ -92,9 +92,11 @@ def parse():
     p.add_argument("--exchange-timeout", type=float, default=300.0,
                    help="seconds the verified full exchange (the first RCCL traffic) may take; "
                         "on expiry as --init-timeout")
-    p.add_argument("--headline-timeout", type=float, default=600.0,
+    p.add_argument("--headline-timeout", type=float, default=240.0,
                    help="seconds the headline measurement (graphs, warmup, timed region, "
-                        "kernel durations) may take; on expiry as --init-timeout")
+                        "kernel durations) may take; on expiry as --init-timeout (a few seconds "
+                        "at the default steps; kept below a 600-s bench limit minus the other "
+                        "stages, so a hang there is still reported)")
     return p.parse_args()
 
 
