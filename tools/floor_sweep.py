@@ -4,7 +4,8 @@ N^3 fp64 domain, halo H, layout_map<2,1,0>, row pitch (N+2H)*8 B) by their own e
 (ghx_launch_timing, medians of 41) beside the address-set floor probes of bench.pack_read_floor
 (tools/pack_floor.hip), over N x H; each shape's exchange is checked cell by cell after the
 timing. One JSON line per shape.
-usage: python tools/floor_sweep.py [N ...]"""
+usage: python tools/floor_sweep.py [--shapes N:H,...] [--tune k=v,k=v ...]
+(each --tune is one setting of ghx_tune keys; the shapes run under each; none = the defaults)"""
 import json
 import os
 import sys
@@ -14,6 +15,15 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="")
+    ap.add_argument("--tune", action="append", default=[])
+    a = ap.parse_args()
+    shapes = [tuple(int(x) for x in sh.split(":")) for sh in a.shapes.split(",") if sh] or \
+        [(N, H) for N in (256, 384, 512, 640) for H in (1, 2, 3)]
+    settings = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in t.split(",") if kv)
+                for t in a.tune] or [{}]
     import torch
     import bench
     import ghex_amd
@@ -22,8 +32,11 @@ def main():
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     L = _ghx.lib()
-    for N in [int(x) for x in sys.argv[1:]] or [256, 384, 512, 640]:
-        for H in (1, 2, 3):
+    for st in settings:
+        _ghx.call("ghx_tune", b"reset", 0)
+        for k, v in st.items():
+            _ghx.call("ghx_tune", k.encode(), v)
+        for N, H in shapes:
             E = N + 2 * H
             ctx = ghex_amd.make_context()
             dd = R.DomainDescriptor(0, (0, 0, 0), (N - 1,) * 3)
@@ -54,7 +67,7 @@ def main():
             fl = bench.pack_read_floor(N, H, roof)
             n = E ** 3 - N ** 3
             print(json.dumps({
-                "N": N, "H": H, "row_pitch_bytes": E * 8, "verified": ok,
+                "tune": st, "N": N, "H": H, "row_pitch_bytes": E * 8, "verified": ok,
                 "pack_us": roof["pack_kernel_us"], "unpack_us": roof["unpack_kernel_us"],
                 "pack_GBps": round(2 * n * 8 / kp / 1e9, 1),
                 "pack_floor_us": fl.get("reads_writes_us"),
