@@ -83,6 +83,30 @@ class _ExchangePlan:
             pass
 
 
+def as_stream(stream, device=None):
+    """The stream argument of schedule_exchange / schedule_wait as a torch stream, accepted in
+    the forms the reference binding accepts (bindings/python/src/_pyghex/unstructured/
+    communication_object.cpp:39-85): None (the current stream), a torch stream, any object with
+    the CUDA stream protocol (`__cuda_stream__()` -> (0, address)) or a `.ptr` (CuPy-style);
+    anything else raises TypeError."""
+    import torch
+    if stream is None:
+        return torch.cuda.current_stream(device)
+    if isinstance(stream, torch.cuda.Stream):
+        return stream
+    if hasattr(stream, "__cuda_stream__"):
+        proto = stream.__cuda_stream__()
+        if not isinstance(proto, tuple) or len(proto) != 2:
+            raise TypeError("Expected a tuple of length 2 from `__cuda_stream__`, got "
+                            f"{proto!r}")
+        if proto[0] != 0:
+            raise TypeError(f"Expected `__cuda_stream__` protocol version 0, but got {proto[0]}")
+        return torch.cuda.ExternalStream(int(proto[1]), device=device)
+    if hasattr(stream, "ptr"):
+        return torch.cuda.ExternalStream(int(stream.ptr), device=device)
+    raise TypeError("Failed to convert the stream object into a CUDA stream.")
+
+
 def _dbl(size):
     """Offset of the odd-parity copy of a double-buffered receive buffer (256-B aligned)."""
     return max(256, (int(size) + 255) // 256 * 256)
@@ -210,7 +234,7 @@ class CommunicationHandle:
         import torch
         if self._event is None or self._co is None:
             return
-        stream = stream if stream is not None else torch.cuda.current_stream(self._stream.device)
+        stream = as_stream(stream, self._stream.device)
         stream.wait_event(self._event)
         ev = torch.cuda.Event()
         ev.record(stream)
@@ -380,10 +404,9 @@ class CommunicationObject:
         """communication_object::schedule_exchange (:287-330): the exchange starts after all
         work submitted to `stream` (None = the current stream) so far, without blocking the
         host; call schedule_wait(stream) on the handle to order later work after the unpack."""
-        import torch
         bis = self._as_list(buffer_infos)
-        if stream is None and bis:
-            stream = torch.cuda.current_stream(bis[0].field.device)
+        if bis:
+            stream = as_stream(stream, bis[0].field.device)
         return self._start(bis, stream)
 
     def _done_event(self, stream):

@@ -82,3 +82,56 @@ def test_is_ready_after_schedule_wait():
     assert h.is_ready()
     assert not co.has_scheduled_exchange()
     np.testing.assert_array_equal(base.cpu().numpy(), H.expected_linear_halo(a, dom, N, Hw, gl))
+
+
+class _ProtocolStream:
+    """An object with the CUDA stream protocol (as the reference test's CUDAStreamProtocolMock)."""
+
+    def __init__(self, s):
+        self._s = s
+
+    def __cuda_stream__(self):
+        return 0, self._s.cuda_stream
+
+
+class _PtrStream:
+    """A CuPy-style stream: the handle in `.ptr`."""
+
+    def __init__(self, s):
+        self.ptr = s.cuda_stream
+
+
+@pytest.mark.parametrize("kind", ["torch", "protocol", "ptr", "none"])
+def test_schedule_exchange_stream_types(kind):
+    """The stream forms the reference binding accepts (test_unstructured_domain_descriptor.py
+    STREAM_TYPES_TO_TEST: None, a CuPy stream, a __cuda_stream__ object): the exchange is
+    ordered after the stream's earlier work and schedule_wait orders later work after it."""
+    import torch
+    from ghex_amd import make_context
+    from ghex_amd.structured import regular as R
+    from tests.gpu_util import device_field
+    N, Hw = 16, 1
+    E = N + 2 * Hw
+    ranks, gf, gl = H.cube_domains(N, (1, 1, 1))
+    dom = ranks[0][0]
+    a, _ = H.linear_index_field(dom, N, Hw, gl)
+    expect = H.expected_linear_halo(a, dom, N, Hw, gl)
+    ctx = make_context()
+    dd = R.DomainDescriptor(0, dom.first, dom.last)
+    pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (True,) * 3), [dd])
+    src = torch.from_numpy(a).cuda()
+    base, logical = device_field(np.full_like(a, -7.0), (2, 1, 0))
+    fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (E,) * 3)
+    co = R.make_communication_object(ctx)
+    s = torch.cuda.Stream() if kind != "none" else torch.cuda.current_stream()
+    arg = {"torch": s, "protocol": _ProtocolStream(s), "ptr": _PtrStream(s), "none": None}[kind]
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(2_000_000)
+        base.copy_(src)
+    h = co.schedule_exchange(arg, [pc(fd)])
+    h.schedule_wait(arg)
+    with torch.cuda.stream(s):
+        got = base.clone()
+    h.wait()
+    s.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy(), expect)

@@ -520,3 +520,26 @@ def test_context_and_config_like_the_reference(thread_safe, capsys):
     assert "transport" in capsys.readouterr().out
     ctx = make_context(None, thread_safe)
     assert ctx.size() == 1 and ctx.rank() == 0
+
+
+def test_stream_argument_forms_refused_like_the_reference():
+    """as_stream refuses what the reference binding's extract_cuda_stream refuses
+    (bindings/python/src/_pyghex/unstructured/communication_object.cpp:39-85)."""
+    from ghex_amd.communication_object import as_stream
+
+    class Bad:
+        pass
+
+    class V1:
+        def __cuda_stream__(self):
+            return 1, 0
+
+    class Short:
+        def __cuda_stream__(self):
+            return (0,)
+    with pytest.raises(TypeError, match="Failed to convert"):
+        as_stream(Bad())
+    with pytest.raises(TypeError, match="version 0"):
+        as_stream(V1())
+    with pytest.raises(TypeError, match="length 2"):
+        as_stream(Short())
