@@ -233,9 +233,8 @@ class FieldDescriptor:
     kind = 0
 
     def __init__(self, domain: DomainDescriptor, field, offsets, extents, num_components=None):
-        import torch
-        if not isinstance(field, torch.Tensor):
-            raise TypeError("field must be a torch.Tensor on the GPU")
+        from ..util import as_device_tensor
+        field = as_device_tensor(field)
         if field.device.type != "cuda":
             raise TypeError("ghex_amd fields live in device memory (torch device 'cuda')")
         D = domain.ndim

@@ -143,8 +143,9 @@ class DataDescriptor:
     kind = 1
 
     def __init__(self, domain: DomainDescriptor, field):
-        import torch
-        if not isinstance(field, torch.Tensor) or field.device.type != "cuda":
+        from .util import as_device_tensor
+        field = as_device_tensor(field)
+        if field.device.type != "cuda":
             raise TypeError("field must be a torch.Tensor in device memory")
         if field.dim() > 2:
             raise TypeError(f"Field has too many dimensions. Expected at most 2, but got {field.dim()}")

@@ -171,3 +171,70 @@ def test_unstructured_domain_descriptor(golden_dir, dtype):
                     else:
                         v = int(got[x, l])
                         assert v - 1000 * int(v / 1000) == 10 * g + l, (r, order, x, v)
+
+
+class _CudaArray:
+    """A producer that exposes only __cuda_array_interface__ (as CuPy / Numba arrays do)."""
+
+    def __init__(self, t):
+        self._t = t
+        self.__cuda_array_interface__ = t.__cuda_array_interface__
+
+
+class _HipArray:
+    """A producer that exposes only __hip_array_interface__."""
+
+    def __init__(self, t):
+        self._t = t
+        self.__hip_array_interface__ = t.__cuda_array_interface__
+
+
+@pytest.mark.parametrize("wrap", [_CudaArray, _HipArray])
+def test_array_interface_fields(wrap):
+    """make_field_descriptor on non-torch device arrays, as the reference binding takes them
+    (__cuda_array_interface__ / __hip_array_interface__, structured/regular.py:66-98 and
+    unstructured.py:38-60): the exchange writes the producer's own memory (zero-copy)."""
+    import numpy as np
+    import torch
+    import ghex_amd
+    from ghex_amd import unstructured as U
+    from ghex_amd.structured import regular as R
+    from tests import helpers as H
+    N, Hw = 12, 2
+    E = N + 2 * Hw
+    ranks, gf, gl = H.cube_domains(N, (1, 1, 1))
+    dom = ranks[0][0]
+    a, _ = H.linear_index_field(dom, N, Hw, gl)
+    expect = H.expected_linear_halo(a, dom, N, Hw, gl)
+    ctx = ghex_amd.make_context()
+    dd = R.DomainDescriptor(0, dom.first, dom.last)
+    pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (True,) * 3), [dd])
+    base = torch.from_numpy(a.copy()).cuda()          # memory order (z, y, x)
+    arr = wrap(base.permute(2, 1, 0))                  # logical (x, y, z), x fastest
+    fd = R.make_field_descriptor(dd, arr, (Hw,) * 3, (E,) * 3)
+    assert fd.tensor.data_ptr() == base.data_ptr()
+    R.make_communication_object(ctx).exchange([pc(fd)]).wait()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(base.cpu().numpy(), expect)
+    # unstructured: one domain whose outer cells are its own inner cells' gids elsewhere in a
+    # second domain of the same rank
+    d0 = U.DomainDescriptor(0, [0, 1, 2, 10], [3])
+    d1 = U.DomainDescriptor(1, [10, 11, 12, 0], [3])
+    upc = U.make_pattern(ctx, U.HaloGenerator(), [d0, d1])
+    v0 = torch.tensor([0.0, 1.0, 2.0, -1.0], device="cuda", dtype=torch.float64)
+    v1 = torch.tensor([10.0, 11.0, 12.0, -1.0], device="cuda", dtype=torch.float64)
+    f0, f1 = U.make_field_descriptor(d0, wrap(v0)), U.make_field_descriptor(d1, wrap(v1))
+    U.make_communication_object(ctx).exchange([upc(f0), upc(f1)]).wait()
+    torch.cuda.synchronize()
+    assert v0.tolist() == [0.0, 1.0, 2.0, 10.0] and v1.tolist() == [10.0, 11.0, 12.0, 0.0]
+
+
+def test_host_arrays_refused():
+    import numpy as np
+    import ghex_amd
+    from ghex_amd.structured import regular as R
+    ctx = ghex_amd.make_context()
+    dd = R.DomainDescriptor(0, (0, 0, 0), (3, 3, 3))
+    with pytest.raises(TypeError, match="host array"):
+        R.make_field_descriptor(dd, np.zeros((6, 6, 6)), (1, 1, 1), (6, 6, 6))
+    del ctx
