@@ -13,6 +13,7 @@ class PatternContainer:
     (pattern_container::operator(), include/ghex/pattern_container.hpp:88-95)."""
 
     grid_type = None  # "structured" | "unstructured"
+    domain_id_type = "int"  # domain ids are int (the bindings' only instantiation)
 
     def __init__(self, handle: int, context, domains, kind: str, dim: int):
         self._h = ctypes.c_void_p(handle)

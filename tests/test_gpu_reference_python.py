@@ -54,6 +54,7 @@ def test_pattern(ndim, periodic, world):
     for r, x in enumerate(ranks):
         ctx = FakeContext(r, world, table)
         pats.append(make_pattern(ctx, halo_gen, [x["dd"]]))
+        assert pats[-1].grid_type == "structured" and pats[-1].domain_id_type == "int"
         cos.append(make_communication_object(ctx))
 
     def make_field(x):
