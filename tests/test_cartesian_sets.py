@@ -180,3 +180,24 @@ def test_halo_gen_call(world, halos):
         assert dd.domain_id() == rank
         assert dd.first() == owned.bounds[0, 0, 0]
         assert dd.last() == owned.bounds[-1, -1, -1]
+
+
+def test_index_space_prune_intersect_and_misc():
+    own = UnitRange(0, 4) * UnitRange(0, 4)
+    sp = IndexSpace({"definition": own, "halo": own.extend(1, 1).without(own),
+                     "nothing": own.without(own)})
+    assert not sp.empty and sp.ndim == 2 and sp.shape == (6, 6)
+    pruned = sp.prune()
+    assert set(pruned.subset) == {"definition", "halo"}
+    cut = sp.intersect(UnitRange(0, 10) * UnitRange(-10, 2))
+    assert cut.subset["definition"] == UnitRange(0, 4) * UnitRange(0, 2)
+    assert set(cut.subset["halo"]) == {p for p in sp.subset["halo"] if p[0] >= 0 and p[1] < 2}
+    assert IndexSpace({"definition": own.without(own)}).empty
+    with pytest.raises(ValueError):
+        IndexSpace({"halo": own})
+    with pytest.deprecated_call():
+        assert own.dim == 2
+    assert hash(own) == hash(UnitRange(0, 4) * UnitRange(0, 4))
+    assert repr(own) == "UnitRange(0, 4) * UnitRange(0, 4)"
+    assert UnitRange(0, 3) * union(UnitRange(0, 1), UnitRange(2, 3)) == \
+        union(UnitRange(0, 3) * UnitRange(0, 1), UnitRange(0, 3) * UnitRange(2, 3))
