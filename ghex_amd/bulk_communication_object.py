@@ -5,7 +5,7 @@ CUDA IPC handles include/ghex/rma/cuda/handle.hpp). SURVEY §8(f) #2.
 Instead of pack -> send -> recv -> unpack, every rank copies its send regions straight into the
 receiving rank's halo cells in peer memory (xGMI on a multi-GPU node), one launch per group of
 up to 64 messages (libghx ghx_put_*: the pack plan of the source side and the unpack plan of the
-target side share one tiling, so a lane moves element p register-to-register). Self messages are
+target side address the same message positions, so a lane moves element p register-to-register). Self messages are
 the same copy inside one field.
 
 Usage mirrors the reference:
@@ -117,6 +117,81 @@ def epochs_error(ep, hosts=None, me=None):
         return (f"{who} failed an epoch wait: its later writes may have overlapped this rank's "
                 f"reads")
     return f"epoch error code {v}"
+
+
+def put_messages(bis, groups, allr, local):
+    """The node-local messages of this rank's fields, as (source field index k, send spaces,
+    target (rank, field index), target spaces): each send halo of field k (domain d, its j-th
+    field) paired with the receive halo of (my domain d, tag) on the target rank's j-th field of
+    the receiving domain (the reference's put ranges, bulk_communication_object.hpp:384-455).
+    bis[k] needs .pattern_container / .local_index; allr[r] = rank r's gathered setup record;
+    groups = _field_groups(); local = the ranks on this host."""
+    target = {}
+    for r, info in enumerate(allr):
+        for i, f in enumerate(info["fields"]):
+            target[(r, f["domain"], f["j"])] = (r, i)
+    msgs = []
+    for k, (bi, (d, j)) in enumerate(zip(bis, groups)):
+        for rid, rr, tag, spaces in bi.pattern_container.send_halos(bi.local_index):
+            if rr not in local:
+                continue  # a remote rank: the buffered exchange carries it
+            key = (rr, rid, j)
+            if key not in target:
+                raise RuntimeError(f"rank {rr} registered no field #{j} for domain {rid}")
+            tr, ti = target[key]
+            tf = allr[tr]["fields"][ti]
+            tsp = next((sp for (sid, stag, sp) in tf["recv"] if sid == d and stag == tag), None)
+            if tsp is None:
+                raise RuntimeError(f"no receive halo on rank {tr} for domain {d}, tag {tag}")
+            msgs.append((k, [(sp[0], sp[1]) for sp in spaces], (tr, ti), tsp))
+    return msgs
+
+
+def put_chunks(msgs):
+    """Messages grouped into put plans (one launch each) of <= 64 messages, <= 64 source and
+    <= 64 target fields: [(chunk, source field indices, target (rank, index) list)]."""
+    out, chunk, srcs, dsts = [], [], [], []
+    for m in msgs + [None]:
+        if (m is None or len(chunk) == MAX_SLOTS or
+                (m[0] not in srcs and len(srcs) == MAX_SLOTS) or
+                (m[2] not in dsts and len(dsts) == MAX_SLOTS)):
+            if chunk:
+                out.append((chunk, srcs, dsts))
+            chunk, srcs, dsts = [], [], []
+            if m is None:
+                break
+        if m[0] not in srcs:
+            srcs.append(m[0])
+        if m[2] not in dsts:
+            dsts.append(m[2])
+        chunk.append(m)
+    return out
+
+
+def put_entries(chunk, srcs, dsts, src_descs, allr):
+    """ghx_put_create's two entry arrays for one chunk: message b is virtual buffer b on both
+    sides; the source side names this rank's fields (src_descs[k]), the target side the
+    target ranks' field descriptors as gathered. Returns (src, dst, keep-alive list)."""
+    n = len(chunk)
+    src = (_ghx.PackEntry * n)()
+    dst = (_ghx.PackEntry * n)()
+    keep = [src, dst]
+    for b, (k, sps, tgt, tsps) in enumerate(chunk):
+        tdesc = _ghx.FieldDesc.from_buffer_copy(allr[tgt[0]]["fields"][tgt[1]]["desc"])
+        for e, desc, slot, spaces in ((src[b], src_descs[k], srcs.index(k), sps),
+                                      (dst[b], tdesc, dsts.index(tgt), tsps)):
+            arr = (_ghx.Box * max(1, len(spaces)))()
+            for i, (lf, ll) in enumerate(spaces):
+                for d in range(len(lf)):
+                    arr[i].first[d], arr[i].last[d] = lf[d], ll[d]
+            keep.append(arr)
+            e.field = desc
+            e.field_slot = slot
+            e.buffer_slot = b
+            e.buffer_offset = 0
+            e.boxes = ctypes.cast(arr, ctypes.POINTER(_ghx.Box))
+            e.n_boxes = len(spaces)
+    return src, dst, keep
 
 
 class BulkHandle:
@@ -243,26 +318,7 @@ class BulkCommunicationObject:
             self._hosts = [info["host"] for info in allr]
             self._ep = attach_epochs(self.context, self._hosts, self.timeout, srcs, tgts)
             self._ep_peers = (srcs, tgts)
-        # target field table: (rank, domain, j) -> (rank, index in that rank's field list)
-        target = {}
-        for r, info in enumerate(allr):
-            for i, f in enumerate(info["fields"]):
-                target[(r, f["domain"], f["j"])] = (r, i)
-        # messages: (src field index k, send spaces, target (rank, i), target spaces)
-        msgs = []
-        for k, (bi, (d, j)) in enumerate(zip(self._bis, groups)):
-            for rid, rr, tag, spaces in bi.pattern_container.send_halos(bi.local_index):
-                if rr not in local:
-                    continue  # a remote rank: the buffered exchange carries it
-                key = (rr, rid, j)
-                if key not in target:
-                    raise RuntimeError(f"rank {rr} registered no field #{j} for domain {rid}")
-                tr, ti = target[key]
-                tf = allr[tr]["fields"][ti]
-                tsp = next((sp for (sid, stag, sp) in tf["recv"] if sid == d and stag == tag), None)
-                if tsp is None:
-                    raise RuntimeError(f"no receive halo on rank {tr} for domain {d}, tag {tag}")
-                msgs.append((k, [(sp[0], sp[1]) for sp in spaces], (tr, ti), tsp))
+        msgs = put_messages(self._bis, groups, allr, local)
         # import peer allocations once per target field
         ptr_of = {}
         for (tr, ti) in sorted({m[2] for m in msgs}):
@@ -275,45 +331,13 @@ class BulkCommunicationObject:
             _ghx.call("ghx_ipc_import", h, f["offset"], ctypes.byref(base), ctypes.byref(ptr))
             self._imports.append(base.value)
             ptr_of[(tr, ti)] = ptr.value
-        # group messages into put plans (one launch each) of <= 64 messages, <= 64 source and
-        # <= 64 target fields
-        chunk, srcs, dsts = [], [], []
-        for m in msgs + [None]:
-            if (m is None or len(chunk) == MAX_SLOTS or
-                    (m[0] not in srcs and len(srcs) == MAX_SLOTS) or
-                    (m[2] not in dsts and len(dsts) == MAX_SLOTS)):
-                if chunk:
-                    self._make_put(chunk, srcs, dsts, allr, ptr_of)
-                chunk, srcs, dsts = [], [], []
-                if m is None:
-                    break
-            if m[0] not in srcs:
-                srcs.append(m[0])
-            if m[2] not in dsts:
-                dsts.append(m[2])
-            chunk.append(m)
+        for chunk, srcs, dsts in put_chunks(msgs):
+            self._make_put(chunk, srcs, dsts, allr, ptr_of)
         self._initialized = True
 
     def _make_put(self, chunk, srcs, dsts, allr, ptr_of):
+        src, dst, keep = put_entries(chunk, srcs, dsts, [bi.field.desc for bi in self._bis], allr)
         n = len(chunk)
-        src = (_ghx.PackEntry * n)()
-        dst = (_ghx.PackEntry * n)()
-        keep = [src, dst]
-        for b, (k, sps, tgt, tsps) in enumerate(chunk):
-            tdesc = _ghx.FieldDesc.from_buffer_copy(allr[tgt[0]]["fields"][tgt[1]]["desc"])
-            for e, desc, slot, spaces in ((src[b], self._bis[k].field.desc, srcs.index(k), sps),
-                                          (dst[b], tdesc, dsts.index(tgt), tsps)):
-                arr = (_ghx.Box * max(1, len(spaces)))()
-                for i, (lf, ll) in enumerate(spaces):
-                    for d in range(len(lf)):
-                        arr[i].first[d], arr[i].last[d] = lf[d], ll[d]
-                keep.append(arr)
-                e.field = desc
-                e.field_slot = slot
-                e.buffer_slot = b
-                e.buffer_offset = 0
-                e.boxes = ctypes.cast(arr, ctypes.POINTER(_ghx.Box))
-                e.n_boxes = len(spaces)
         h = ctypes.c_void_p()
         _ghx.call("ghx_put_create", src, n, dst, n, ctypes.byref(h))
         sp = _ghx.ptr_array([self._bis[k].field.data_ptr() for k in srcs])

@@ -243,22 +243,22 @@ const char* get_error() { return g_error.c_str(); }
 }  // namespace ghx
 
 // Put plan: the pack plan of the source side and the unpack plan of the target side, segment k
-// of each covering the same virtual message bytes with the same tiling (checked).
+// of each covering the same virtual message bytes (checked). The launch is tiled by the source
+// plan's tile table alone (k_put addresses the target segment by message position), so the
+// target plan's own tiling is not compared: the two sides size their short-row tiles by their
+// own fields' rows (one source field, one target field per peer) and differ at large sizes.
 struct ghx_put
 {
     std::unique_ptr<ghx::splan> from, to;
     ghx_put(const ghx_pack_entry* src, int n_src, const ghx_pack_entry* dst, int n_dst)
     : from(new ghx::splan(src, n_src, 0)), to(new ghx::splan(dst, n_dst, 1))
     {
-        bool ok = from->host_segs.size() == to->host_segs.size() && from->n_tiles == to->n_tiles &&
-                  from->bytes == to->bytes;
+        bool ok = from->host_segs.size() == to->host_segs.size() && from->bytes == to->bytes;
         for (size_t k = 0; ok && k < from->host_segs.size(); ++k)
         {
             const auto& a = from->host_segs[k];
             const auto& b = to->host_segs[k];
-            ok = a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
-                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes &&
-                 a.n_outer == b.n_outer;
+            ok = ghx::exchange_plan::same_message(a, b) && a.n_outer == b.n_outer;
             for (int d = 0; ok && d < 4; ++d) ok = a.ext[d] == b.ext[d];
         }
         if (!ok)
@@ -448,9 +448,7 @@ void build_mixed(exchange_plan& ex, int32_t me, const std::vector<ghx_pack_entry
         short_self = short_self || ps[k].row_bytes < g_tune.small_row_bytes;
         if (m >= su.host_segs.size()) return;
         const seg_s& q = su.host_segs[m++];
-        if (q.buf_slot != ps[k].buf_slot || q.buf_off != ps[k].buf_off || q.bytes != ps[k].bytes ||
-            q.row_bytes != ps[k].row_bytes || q.tile_bytes != ps[k].tile_bytes || q.bytes == 0)
-            return;
+        if (!exchange_plan::same_message(ps[k], q) || q.bytes == 0) return;
         comp[k] = q;
     }
     if (m != su.host_segs.size()) return;
@@ -1000,7 +998,7 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
                     std::make_unique<uplan>(uent.data(), int(uent.size()), receive ? 1 : 0);
         }
         if (!ex->self_fusable() || !ex->self_pack || !ex->self_unpack ||
-            !exchange_plan::same_tiling(*ex->self_pack, *ex->self_unpack))
+            !exchange_plan::same_messages(*ex->self_pack, *ex->self_unpack))
         {
             ex->self_pack.reset();
             ex->self_unpack.reset();

@@ -109,22 +109,30 @@ struct exchange_plan
         for (size_t i = 0; ok && i < send.size(); ++i)
             ok = send[i].first_id == recv[i].first_id && send[i].second_id == recv[i].second_id &&
                  send[i].size == recv[i].size;
-        if (ok) ok = same_tiling(*spack, *sunpack);
+        if (ok) ok = same_messages(*spack, *sunpack);
         self_ok = ok ? 1 : 0;
         return ok;
     }
 
-    // pack segment k and unpack segment k cover the same buffer bytes with the same tiling
-    static bool same_tiling(const splan& p, const splan& q)
+    // Segment a of a launch's primary plan and its companion b (the unpack side of a fused self
+    // tile, the target side of a put) cover the same buffer bytes with the same rows. Tiling is
+    // deliberately not compared: a fused launch (k_self, k_put) runs the primary plan's tile
+    // table and reads only a's tile_bytes, and the two sides size their short-row tiles from
+    // different fields' row counts (a put's one source field vs one target field per peer; the
+    // mixed pairing's self messages vs every message of the field), which differ once a field
+    // holds more than the 512-row minimum's worth (512^3 (2,2,1) puts refused).
+    static bool same_message(const seg_s& a, const seg_s& b)
     {
-        bool ok = p.host_segs.size() == q.host_segs.size() && p.n_tiles == q.n_tiles;
+        return a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
+               a.row_bytes == b.row_bytes;
+    }
+
+    // pack segment k and unpack segment k cover the same buffer bytes (same_message)
+    static bool same_messages(const splan& p, const splan& q)
+    {
+        bool ok = p.host_segs.size() == q.host_segs.size();
         for (size_t k = 0; ok && k < p.host_segs.size(); ++k)
-        {
-            const auto& a = p.host_segs[k];
-            const auto& b = q.host_segs[k];
-            ok = a.buf_slot == b.buf_slot && a.buf_off == b.buf_off && a.bytes == b.bytes &&
-                 a.row_bytes == b.row_bytes && a.tile_bytes == b.tile_bytes;
-        }
+            ok = same_message(p.host_segs[k], q.host_segs[k]);
         return ok;
     }
 };

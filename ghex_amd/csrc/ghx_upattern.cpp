@@ -209,6 +209,20 @@ struct ghx_upattern
     {
         return int32_t((src_local << shift) | unsigned(tgt));
     }
+
+    // Two halos of one local domain with one peer rank under the same tag: the reference's tag
+    // layout (src_local << num_bits(max_num_domains)) | dst_id (unstructured/pattern.hpp:
+    // 230-232) cannot tell them apart once a domain id needs more than `shift` bits and a rank
+    // holds several domains. The reference's map insert keeps the first and drops the other
+    // (its exchange then hangs or moves wrong data); here setup fails on the rank that sees it.
+    std::string collision(int32_t local_id, int32_t peer, int32_t tag) const
+    {
+        return "unstructured make_pattern: two halos of domain " + std::to_string(local_id) +
+               " with rank " + std::to_string(peer) + " share tag " + std::to_string(tag) +
+               " (tag = source index << " + std::to_string(shift) +
+               " | target domain id: with several domains per rank, domain ids must be below " +
+               std::to_string(1u << shift) + ")";
+    }
 };
 
 namespace
@@ -340,7 +354,8 @@ int ghx_upattern_add_halos(ghx_upattern* b, int32_t rank, int32_t n_domains,
                     }
                 if (e.lids.empty()) continue;
                 e.key = {domain_ids[k], rank, tag};
-                if (!b->send[i].emplace(std::make_pair(rank, tag), std::move(e)).second) continue;
+                if (!b->send[i].emplace(std::make_pair(rank, tag), std::move(e)).second)
+                    throw std::runtime_error(b->collision(d.id, rank, tag));
                 b->records.push_back({d.id, domain_ids[k], rank, tag, std::move(g)});
             }
             off += halo_sizes[k];
@@ -383,7 +398,8 @@ int ghx_upattern_add_recv(ghx_upattern* b, int32_t src_rank, int32_t src_id, int
                 throw std::runtime_error("received halo gids that are not outer cells of domain " +
                                          std::to_string(dst_id));
             e.key = {src_id, src_rank, tag};
-            b->recv[i].emplace(std::make_pair(src_rank, tag), std::move(e));
+            if (!b->recv[i].emplace(std::make_pair(src_rank, tag), std::move(e)).second)
+                throw std::runtime_error(b->collision(dst_id, src_rank, tag));
             return GHX_OK;
         }
         throw ghx::invalid("no local domain with id " + std::to_string(dst_id));

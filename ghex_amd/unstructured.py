@@ -73,6 +73,19 @@ class HaloGenerator:
         return cls(gids)
 
 
+def _agree(context, err, stage):
+    """Every rank learns whether any rank failed at this setup stage (one all_gather of a short
+    string): all raise together instead of the healthy ranks blocking in the next collective
+    (ADVICE r05). A failing rank re-raises its own error; the others name the first failure."""
+    why = context.all_gather_object(None if err is None else f"{type(err).__name__}: {err}")
+    if err is not None:
+        raise err
+    bad = [(r, w) for r, w in enumerate(why) if w]
+    if bad:
+        raise RuntimeError(f"make_pattern<unstructured> ({stage}): rank {bad[0][0]} failed: "
+                           f"{bad[0][1]}")
+
+
 def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[DomainDescriptor]):
     """make_pattern<unstructured::grid> (include/ghex/unstructured/pattern.hpp:187-370), the
     reference's reduced-halo algorithm: this rank passes only its own domains; the ranks
@@ -94,23 +107,36 @@ def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[Domain
     max_n = max(m[1] for m in meta)
     handles = (ctypes.c_void_p * len(doms))(*[d._h.value for d in doms])
     b = ctypes.c_void_p()
-    _ghx.call("ghx_upattern_create", handles, len(doms), me, max_n, max_id, ctypes.byref(b))
+    err = None
     try:
+        _ghx.call("ghx_upattern_create", handles, len(doms), me, max_n, max_id, ctypes.byref(b))
         # reduced halos of my domains: [n, ids..., sizes..., gids...] (:243-254)
         halos = [d.halo_gids(halo_gen) for d in doms]
         payload = np.concatenate([np.array([len(doms)], np.int64), np.array(ids, np.int64),
                                   np.array([h.size for h in halos], np.int64)] + halos)
+    except Exception as e:  # every rank learns of it below, none is left in the ring
+        err, payload = e, np.zeros(1, np.int64)
+    _agree(context, err, "setup")
+    p = ctypes.c_void_p()
+    try:
         n_rec = ctypes.c_int64()
         # every rank's reduced halos, around the ring, against my inner gids -> send halos
-        # (:284-330; at most two ranks' halos held at a time)
+        # (:284-330; at most two ranks' halos held at a time). A rank that fails on one step
+        # keeps passing the arrays on, so its peers finish the ring and all raise together.
         for r, arr in context.ring_arrays(payload):
-            k = int(arr[0])
-            rid = np.ascontiguousarray(arr[1:1 + k], dtype=np.int32)
-            sizes = np.ascontiguousarray(arr[1 + k:1 + 2 * k])
-            gids = np.ascontiguousarray(arr[1 + 2 * k:])
-            _ghx.call("ghx_upattern_add_halos", b, r, k,
-                      rid.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _ghx.i64_ptr(sizes),
-                      _ghx.i64_ptr(gids), ctypes.byref(n_rec))
+            if err is not None:
+                continue
+            try:
+                k = int(arr[0])
+                rid = np.ascontiguousarray(arr[1:1 + k], dtype=np.int32)
+                sizes = np.ascontiguousarray(arr[1 + k:1 + 2 * k])
+                gids = np.ascontiguousarray(arr[1 + 2 * k:])
+                _ghx.call("ghx_upattern_add_halos", b, r, k,
+                          rid.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                          _ghx.i64_ptr(sizes), _ghx.i64_ptr(gids), ctypes.byref(n_rec))
+            except Exception as e:
+                err = e
+        _agree(context, err, "send halos")
         recs, sends = [], []
         f = [ctypes.c_int32() for _ in range(4)]
         n = ctypes.c_int64()
@@ -125,13 +151,23 @@ def make_pattern(context, halo_gen: HaloGenerator, domain_range: Sequence[Domain
         every = context.all_gather_object(recs)
         mine = [(src, rec) for src, rs in enumerate(every) for rec in rs if rec[2] == me]
         got = context.exchange_arrays(sends, [(src, rec[4]) for src, rec in mine])
-        for (src, (src_id, dst_id, _, tag, cnt)), g in zip(mine, got):
-            g = np.ascontiguousarray(g, dtype=np.int64)
-            _ghx.call("ghx_upattern_add_recv", b, src, src_id, dst_id, tag, _ghx.i64_ptr(g), cnt)
-        p = ctypes.c_void_p()
-        _ghx.call("ghx_upattern_finish", b, ctypes.byref(p))
+        try:
+            for (src, (src_id, dst_id, _, tag, cnt)), g in zip(mine, got):
+                g = np.ascontiguousarray(g, dtype=np.int64)
+                _ghx.call("ghx_upattern_add_recv", b, src, src_id, dst_id, tag, _ghx.i64_ptr(g),
+                          cnt)
+            _ghx.call("ghx_upattern_finish", b, ctypes.byref(p))
+        except Exception as e:
+            err = e
+        try:
+            _agree(context, err, "receive halos")
+        except Exception:
+            if p.value:
+                _ghx.lib().ghx_pattern_destroy(p)
+            raise
     finally:
-        _ghx.lib().ghx_upattern_destroy(b)
+        if b.value:
+            _ghx.lib().ghx_upattern_destroy(b)
     return PatternContainer(p.value, context, doms, "unstructured", 1)
 
 

@@ -15,13 +15,18 @@
 // the indices resident in device memory (the reference reads them from managed memory).
 //
 // Plans: the first pack/unpack of an index list uploads it once (ghx_uplan_create); later calls
-// with the same list find the plan by the list's address, length and index width and check 16
-// sampled entries (O(1) host work per call; a list rebuilt at the same address, e.g. by a new
-// pattern, differs there almost surely and gets a new plan). This relies on the reference's
-// contract that the pattern's index containers are immutable and outlive every exchange that
-// uses them (include/ghex/pattern_container.hpp:84-87); call forget_plans() after changing a list
-// in place. Copies of a descriptor share its plans (guarded by a mutex). (The plain C entry
-// points ghx_unstructured_pack/unpack compare the whole list on every call instead.)
+// with the same list find the plan by the list's address, length and index width, and confirm
+// the list is unchanged by comparing it with a host copy kept with the plan (a memcmp: exact, so
+// a list rebuilt at a freed list's address, e.g. by a new pattern, always gets a new plan; about
+// 30 us per 500k-entry list, tools/udata_cost.hip). A caller that keeps the reference's contract —
+// the pattern's index containers are immutable and outlive every exchange that uses them
+// (include/ghex/pattern_container.hpp:84-87) — may call assume_immutable_index_lists(true):
+// then 16 sampled entries are compared instead (O(1) host work per call), and a list changed in
+// place, or rebuilt at the same address, needs forget_plans(). At most max_plans() plans are
+// kept (least recently used dropped first; each holds a device copy of its list), so rebuilding
+// patterns does not grow device memory without bound. Copies of a descriptor share its plans
+// (guarded by a mutex). (The plain C entry points ghx_unstructured_pack/unpack compare the whole
+// list on every call too.)
 //
 // Depends only on <ghx.h> and the standard library; link with -lghx.
 #pragma once
@@ -30,6 +35,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -73,12 +79,17 @@ class data_descriptor
     struct cached
     {
         std::shared_ptr<ghx_uplan> plan;
-        int64_t sample[kSamples];  // entries at i * (n - 1) / (kSamples - 1)
+        std::vector<char> content;  // the list's bytes (exact check), empty in sampled mode
+        int64_t sample[kSamples];   // entries at i * (n - 1) / (kSamples - 1)
+        uint64_t used = 0;          // LRU stamp
     };
     struct plan_cache
     {
         std::mutex mtx;
         std::map<plan_key, cached> map;
+        uint64_t clock = 0;
+        std::size_t max_plans = 64;
+        bool trust = false;  // assume_immutable_index_lists
     };
     std::shared_ptr<plan_cache> m_plans = std::make_shared<plan_cache>();
 
@@ -136,31 +147,74 @@ class data_descriptor
             run(is.local_indices(), 1, const_cast<value_type*>(buffer), stream_ptr);
     }
 
-    // drop the cached plans (after an index list was changed in place)
+    // drop the cached plans (after an index list was changed in place, in sampled mode)
     void forget_plans()
     {
         std::lock_guard<std::mutex> g(m_plans->mtx);
         m_plans->map.clear();
     }
 
+    // true: trust the reference's contract that index lists are immutable while cached and
+    // check 16 sampled entries per call instead of the whole list (see the header comment)
+    void assume_immutable_index_lists(bool on)
+    {
+        std::lock_guard<std::mutex> g(m_plans->mtx);
+        if (on != m_plans->trust) m_plans->map.clear();  // entries carry the other mode's check
+        m_plans->trust = on;
+    }
+
+    // plans kept at most (least recently used dropped first); >= 1
+    void set_max_plans(std::size_t n)
+    {
+        std::lock_guard<std::mutex> g(m_plans->mtx);
+        m_plans->max_plans = std::max<std::size_t>(1, n);
+        evict();
+    }
+    std::size_t max_plans() const { return m_plans->max_plans; }
+    std::size_t num_plans() const
+    {
+        std::lock_guard<std::mutex> g(m_plans->mtx);
+        return m_plans->map.size();
+    }
+
   private:
+    // drop least recently used plans beyond the bound (caller holds the mutex); a plan still
+    // referenced by a running call stays alive through its shared_ptr
+    void evict()
+    {
+        auto& m = m_plans->map;
+        while (m.size() > m_plans->max_plans)
+            m.erase(std::min_element(m.begin(), m.end(), [](const auto& a, const auto& b) {
+                return a.second.used < b.second.used;
+            }));
+    }
+
     template<typename V>
     void run(const V& l, int32_t dir, value_type* buffer, void* stream_ptr)
     {
         if (l.empty()) return;
         const plan_key key{static_cast<const void*>(l.data()), l.size(), lid_bytes(l), dir};
+        const std::size_t nbytes = l.size() * std::size_t(lid_bytes(l));
+        const char* raw = reinterpret_cast<const char*>(l.data());
         int64_t sample[kSamples];
         for (int i = 0; i < kSamples; ++i)
             sample[i] = int64_t(l[(l.size() - 1) * std::size_t(i) / (kSamples - 1)]);
         std::shared_ptr<ghx_uplan> plan;  // held: a concurrent forget_plans() cannot free it
         {
             std::lock_guard<std::mutex> g(m_plans->mtx);
+            const bool trust = m_plans->trust;
             auto it = m_plans->map.find(key);
-            if (it != m_plans->map.end() &&
-                !std::equal(sample, sample + kSamples, it->second.sample))
+            if (it != m_plans->map.end())
             {
-                m_plans->map.erase(it);  // a different list at the same address
-                it = m_plans->map.end();
+                const cached& c = it->second;
+                const bool same = trust ? std::equal(sample, sample + kSamples, c.sample)
+                                        : c.content.size() == nbytes &&
+                                              std::memcmp(c.content.data(), raw, nbytes) == 0;
+                if (!same)
+                {
+                    m_plans->map.erase(it);  // a different list at the same address
+                    it = m_plans->map.end();
+                }
             }
             if (it == m_plans->map.end())
             {
@@ -176,10 +230,13 @@ class data_descriptor
                 check_u(ghx_uplan_create(&e, 1, dir, &p), "ghx_uplan_create");
                 cached c;
                 c.plan.reset(p, ghx_uplan_destroy);
+                if (!trust) c.content.assign(raw, raw + nbytes);
                 std::copy(sample, sample + kSamples, c.sample);
                 it = m_plans->map.emplace(key, std::move(c)).first;
             }
+            it->second.used = ++m_plans->clock;
             plan = it->second.plan;
+            evict();
         }
         void* f[1] = {m_values};
         void* b[1] = {buffer};

@@ -97,6 +97,14 @@ static int64_t batch_is(const orc_field* f, char* field, char* buf, const int32_
     }
     int32_t x[ORC_MAXD];
     for (int d = 0; d < D; ++d) x[d] = first[d];
+    /* the innermost loop of the nest (layout value D-2) runs with pointer increments, as the
+     * reference's compile-time for_loop lets the compiler do; the outer ones as an odometer.
+     * Same rows in the same order (tools/cpu_serializer_ab.cpp: 1.15-1.2x faster than
+     * recomputing every row's offsets, profiles/r06_cpu_ab.jsonl). */
+    const int in = no > 0 ? order[no - 1] : -1;
+    const int64_t n_in = in >= 0 ? ext[in] : 1;
+    const int64_t fs_in = in >= 0 ? f->fstride[in] : 0, bs_in = in >= 0 ? bs[in] : 0;
+    const size_t rb = (size_t)row_bytes;
     for (;;)
     {
         int64_t foff = 0, boff = 0;
@@ -105,10 +113,14 @@ static int64_t batch_is(const orc_field* f, char* field, char* buf, const int32_
             foff += ((int64_t)x[d] + f->offset[d]) * f->fstride[d];
             boff += ((int64_t)x[d] - first[d]) * bs[d];
         }
-        if (dir == 0) memcpy(buf + boff, field + foff, (size_t)row_bytes);
-        else memcpy(field + foff, buf + boff, (size_t)row_bytes);
-        /* advance odometer, innermost = order[no-1] */
-        int k = no - 1;
+        char* fp = field + foff;
+        char* bp = buf + boff;
+        if (dir == 0)
+            for (int64_t i = 0; i < n_in; ++i, fp += fs_in, bp += bs_in) memcpy(bp, fp, rb);
+        else
+            for (int64_t i = 0; i < n_in; ++i, fp += fs_in, bp += bs_in) memcpy(fp, bp, rb);
+        /* advance the odometer over the outer dims, order[no-2] fastest */
+        int k = no - 2;
         for (; k >= 0; --k)
         {
             int d = order[k];

@@ -4,7 +4,9 @@
 // Usage: udata_demo n_cells levels levels_first lid_bytes(4|8) lids_file out_prefix
 //   lids_file: int64 local indices; values[i, l] = i*100 + l before the pack;
 //   writes <out>.buf (packed buffer), <out>.values (after unpacking buffer[k] = 1e6 + k) and
-//   <out>.buf2 (the list reversed in place, packed again from those values).
+//   <out>.buf2 (the list reversed in place, packed again from those values), <out>.buf3 (then
+//   entries 1 and 2 swapped in place, packed again) and <out>.plans (plans kept after 5 more
+//   lists through a cache bounded at 2).
 #include <hip/hip_runtime.h>
 
 #include <ghex_amd/data_descriptor.hpp>
@@ -71,6 +73,24 @@ int run(size_t n, int levels, bool lf, const std::vector<int64_t>& lids, const c
     HCK(hipMemcpy(hb.data(), buf, nb * 8, hipMemcpyDeviceToHost));
     std::ofstream(std::string(out) + ".buf2", std::ios::binary)
         .write(reinterpret_cast<const char*>(hb.data()), std::streamsize(nb * 8));
+    // entries 1 and 2 swapped in place: positions no sample covers (the sampled
+    // check missed such a change); the exact check must build a new plan
+    if (c[0].m_lids.size() > 2) std::swap(c[0].m_lids[1], c[0].m_lids[2]);
+    d.pack(buf, c, &s);
+    HCK(hipStreamSynchronize(s));
+    HCK(hipMemcpy(hb.data(), buf, nb * 8, hipMemcpyDeviceToHost));
+    std::ofstream(std::string(out) + ".buf3", std::ios::binary)
+        .write(reinterpret_cast<const char*>(hb.data()), std::streamsize(nb * 8));
+    // the cache stays bounded: 5 distinct lists through a cache of at most 2 plans
+    d.set_max_plans(2);
+    std::vector<iteration_space<I>> more(1);
+    for (int k = 0; k < 5; ++k)
+    {
+        more[0].m_lids.assign(c[0].m_lids.begin(), c[0].m_lids.begin() + 1 + k);
+        d.pack(buf, more, &s);
+    }
+    HCK(hipStreamSynchronize(s));
+    std::ofstream(std::string(out) + ".plans") << d.num_plans() << "\n";
     HCK(hipFree(values));
     HCK(hipFree(buf));
     HCK(hipStreamDestroy(s));

@@ -88,3 +88,11 @@ def test_cpp_unstructured_adaptor(tmp_path, levels, levels_first, lid_bytes):
     ob2 = np.zeros(len(lids) * levels * 8, np.uint8)
     orc.unstructured_get(exp, ob2, 8, lids[::-1].copy(), levels, levels_first, isd, lsd)
     np.testing.assert_array_equal(np.fromfile(pre + ".buf2", dtype=np.uint8), ob2)
+    # then entries 1 and 2 swapped in place, between the 16 sampled positions:
+    # the exact check builds a new plan
+    rl = lids[::-1].copy()
+    rl[[1, 2]] = rl[[2, 1]]
+    ob3 = np.zeros(len(lids) * levels * 8, np.uint8)
+    orc.unstructured_get(exp, ob3, 8, rl, levels, levels_first, isd, lsd)
+    np.testing.assert_array_equal(np.fromfile(pre + ".buf3", dtype=np.uint8), ob3)
+    assert int(open(pre + ".plans").read()) == 2  # LRU bound held

@@ -122,3 +122,14 @@ def test_race_check_sees_a_missing_epoch():
     """Negative control of the race checks: the direct race loop with the epoch launch left out
     must report cells of other exchanges (profiles/r04_epoch_soak.json: 41M bad cells at 500)."""
     _run((2, 2, 1), 12, 3, "directnoepoch", reps=50, jitter=True, expect_bad=True)
+
+
+@pytest.mark.parametrize("mode", ["bulk", "direct"])
+def test_zero_copy_beyond_the_short_row_tile_minimum(mode):
+    """the zero-copy forms at a size where the per-field short-row tile rule
+    leaves its 512-row minimum (256^3 H=2: 133k short rows per field, 1024-row tiles on the
+    source side, 512 on a diagonal peer's target side). Round 5's put plan compared the two
+    sides' tilings and refused it (ghx_put_create failed at 512^3 in the N=4 rehearsal while
+    every N <= 16 case here passed); host-side planning of the same pairs at 256^3 / 512^3 is in
+    tests/test_plan_pairing.py."""
+    _run((2, 2, 1), 256, 2, mode, reps=2)

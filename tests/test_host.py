@@ -543,3 +543,32 @@ def test_stream_argument_forms_refused_like_the_reference():
         as_stream(V1())
     with pytest.raises(TypeError, match="length 2"):
         as_stream(Short())
+
+
+def test_unstructured_tag_collision_fails_on_every_rank():
+    """with several domains per rank the reference's tag layout
+    (src_local << num_bits(max domains per rank)) | dst_id (unstructured/pattern.hpp:230-232)
+    repeats a tag once a domain id needs more bits: here shift = num_bits(2) = 3, and rank 0's
+    second domain (local index 1) sends to rank 1's domains 8 and 0 under tag
+    (1 << 3) | 8 == (1 << 3) | 0 == 8.
+    The reference's map keeps one of the two halos and the exchange hangs or moves wrong data;
+    here setup fails, on every rank (the others do not wait in the ring or a later collective)."""
+    from ghex_amd.context import LoopbackWorld
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
+    ranks = [[(1, list(range(0, 10)), []), (2, list(range(10, 20)), [])],
+             [(8, list(range(20, 30)) + [10], [10]), (0, list(range(30, 40)) + [11], [10])]]
+    errs = []
+
+    def rank_fn(ctx):
+        try:
+            make_pattern(ctx, HaloGenerator(), [DomainDescriptor(i, g, o) for i, g, o in ranks[ctx.rank()]])
+        except Exception as e:
+            errs.append((ctx.rank(), str(e)))
+            return "raised"
+        return "returned"
+
+    assert LoopbackWorld(2).run(rank_fn) == ["raised", "raised"]
+    assert any("share tag 8" in e for _, e in errs), errs
+    # the same halos with domain ids below 1 << shift are fine
+    ranks[1][0] = (3,) + ranks[1][0][1:]
+    assert LoopbackWorld(2).run(rank_fn) == ["returned", "returned"]
