@@ -1313,7 +1313,7 @@ def pack_read_floor(N, Hw, roof):
         L = _floor_lib()
         if L is None:
             return {"error": "tools/lib/libpackfloor.so not built (make -C tools)"}
-        us = (ctypes.c_double * 8)()
+        us = (ctypes.c_double * 10)()
         c = (ctypes.c_int64 * 3)()
         rc = L.ghx_probe_pack_floor(N, Hw, 21, us, c)
         if rc:
@@ -1329,13 +1329,19 @@ def pack_read_floor(N, Hw, roof):
         if rc:
             out["write_floor"] = {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
         else:
+            # the floor: the faster of the two buffer-read arrangements (streamed first, or
+            # interleaved with the writes as the unpack kernel issues them)
+            fl = min(us[6], us[8])
             out["write_floor"] = {
                 "xface_pieces": c[0], "long_pieces": c[1],
                 "xface_writes_us": round(us[0], 2), "long_writes_us": round(us[2], 2),
                 "writes_us": round(us[4], 2), "writes_reads_us": round(us[6], 2),
                 "writes_reads_cold_us": round(us[7], 2),
+                "writes_reads_interleaved_us": round(us[8], 2),
+                "writes_reads_interleaved_cold_us": round(us[9], 2),
+                "floor_us": round(fl, 2),
                 "unpack_kernel_us": roof.get("unpack_kernel_us"),
-                "floor_over_kernel": round(us[6] / roof["unpack_kernel_us"], 3)
+                "floor_over_kernel": round(fl / roof["unpack_kernel_us"], 3)
                 if roof.get("unpack_kernel_us") else None}
         return out
     except Exception as e:  # reported, never fatal

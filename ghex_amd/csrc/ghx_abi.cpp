@@ -500,6 +500,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 1) throw invalid("mixed_always must be 0 or 1");
             g_tune.mixed_always = value;
         }
+        else if (k == "tile_records")
+        {
+            if (value < 0 || value > 1) throw invalid("tile_records must be 0 or 1");
+            g_tune.tile_records = value;
+        }
         else if (k == "xcd_pair")
         {
             if (value < 0 || value > 1) throw invalid("xcd_pair must be 0 or 1");

@@ -56,6 +56,9 @@ struct tuning
                                        // round-robin over the 8 XCDs) at the same time
     int mixed_always = 0;              // build the mixed self/peer plans even when the self
                                        // messages hold no short rows (tests, measurements)
+    int tile_records = 1;              // k_copy reads per tile ONE record (its segment with the
+                                       // tile index in first_tile) at blockIdx: no dependent
+                                       // tile-table load ahead of the segment load
 };
 extern tuning g_tune;
 
@@ -92,7 +95,8 @@ struct alignas(16) seg_s
     magic_u32 mag_ext[3]; // division by ext[0], ext[1], ext[2]
     uint32_t row_bytes;   // L: bytes per contiguous run
     uint32_t bytes;       // rows * L
-    uint32_t first_tile;  // first tile index of this segment
+    uint32_t first_tile;  // 0 in a segment table; in a tile record, the tile's index in its
+                          // segment
     uint16_t field_slot;
     uint16_t buf_slot;
     uint8_t wlog2;        // log2 of the widest vector (<= 16 B) that divides L, offsets, strides
@@ -142,6 +146,7 @@ struct kargs
     const void* segs;
     const void* segs2;         // fused self exchange: the unpack segments (1:1 with segs)
     const uint32_t* tile_seg;  // per tile: {segment index, tile index within the segment}
+    const void* tile_recs;     // or per tile one record (k_copy; null: use segs + tile_seg)
     uint32_t n_tiles;
     uint32_t parity_add;       // double-buffered launches: parity = (*parity_word + add) & 1
     const uint64_t* parity_word;  // null: single-buffered (the kernels' plain variants)

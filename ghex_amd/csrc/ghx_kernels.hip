@@ -526,17 +526,32 @@ __device__ __forceinline__ bool odd_parity(const kargs& a)
              a.parity_add) & 1) != 0;
 }
 
-template<bool PACK, typename Seg, bool RUNS = false, bool DBL = false, int UU = kU>
+// REC (tile records, g_tune.tile_records): the workgroup's first load is its own record at
+// tile_recs[blockIdx.x] (the segment, with the tile's index in first_tile), so the chain ahead
+// of the first data load is one table load instead of tile table -> segment. The grid never
+// exceeds n_tiles (grid_for_tiles), so the first tile needs no bound check either.
+template<bool PACK, typename Seg, bool RUNS = false, bool DBL = false, int UU = kU, bool REC = false>
 __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
 {
-    const Seg* __restrict__ segs = static_cast<const Seg*>(a.segs);
+    const Seg* __restrict__ segs = static_cast<const Seg*>(REC ? a.tile_recs : a.segs);
     bool odd = false;
     if constexpr (DBL) odd = odd_parity(a);
-    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
+    uint32_t t = blockIdx.x;
+    do
     {
-        const uint32_t si = a.tile_seg[2 * t];
-        const uint32_t ti = a.tile_seg[2 * t + 1];
-        const Seg s = segs[si];
+        Seg s;
+        uint32_t ti;
+        if constexpr (REC)
+        {
+            s = segs[t];
+            ti = s.first_tile;
+        }
+        else
+        {
+            const uint32_t si = a.tile_seg[2 * t];
+            ti = a.tile_seg[2 * t + 1];
+            s = segs[si];
+        }
         const uint32_t start = ti * s.tile_bytes;
         const uint32_t end = min(start + s.tile_bytes, s.bytes);
         char* field = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
@@ -547,13 +562,16 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
         {
             if (s.row_bytes == 8) copy_runs<PACK, 8>(s, field, buf, start, end);
             else copy_runs<PACK, 4>(s, field, buf, start, end);
-            continue;
         }
-        int w = s.wlog2;
-        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
-        w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
-        copy_any<PACK, UU>(s, field, buf, start, end, w);
-    }
+        else
+        {
+            int w = s.wlog2;
+            w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(field)));
+            w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(buf)));
+            copy_any<PACK, UU>(s, field, buf, start, end, w);
+        }
+        t += gridDim.x;
+    } while (t < a.n_tiles);
 }
 
 // Lane-local self tile with store-to-load forwarding: the unpack half needs exactly the buffer
@@ -779,17 +797,25 @@ uint32_t grid_for_tiles(uint32_t n_tiles)
     return n_tiles < cap ? n_tiles : cap;
 }
 
+template<bool REC>
+void launch_s(const kargs& a, int direction, hipStream_t s, uint32_t grid)
+{
+    if (a.parity_word)
+    {
+        if (direction == 0) launch((k_copy<true, seg_s, false, true, kU, REC>), grid, s, a);
+        else launch((k_copy<false, seg_s, false, true, kU, REC>), grid, s, a);
+    }
+    else if (direction == 0) launch((k_copy<true, seg_s, false, false, kU, REC>), grid, s, a);
+    else launch((k_copy<false, seg_s, false, false, kU, REC>), grid, s, a);
+}
+
 int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid)
 {
     if (a.n_tiles == 0) return GHX_OK;
+    grid = min(grid, a.n_tiles);  // k_copy's first tile is unchecked: never more groups than tiles
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (a.parity_word)
-    {
-        if (direction == 0) launch((k_copy<true, seg_s, false, true>), grid, s, a);
-        else launch((k_copy<false, seg_s, false, true>), grid, s, a);
-    }
-    else if (direction == 0) launch((k_copy<true, seg_s>), grid, s, a);
-    else launch((k_copy<false, seg_s>), grid, s, a);
+    if (a.tile_recs) launch_s<true>(a, direction, s, grid);
+    else launch_s<false>(a, direction, s, grid);
     return launched("structured");
 }
 
@@ -808,26 +834,27 @@ int launch_put(const kargs& a, void* stream, uint32_t grid)
     return launched("put");
 }
 
-template<bool DBL>
-void launch_u_general(const kargs& a, int direction, hipStream_t s, uint32_t grid)
+template<bool DBL, bool REC>
+void launch_u(const kargs& a, int direction, hipStream_t s, uint32_t grid, bool runs)
 {
-    if (direction == 0) launch((k_copy<true, seg_u, false, DBL>), grid, s, a);
-    else launch((k_copy<false, seg_u, false, DBL>), grid, s, a);
+    if (runs && direction == 0) launch((k_copy<true, seg_u, true, DBL, kU, REC>), grid, s, a);
+    else if (runs) launch((k_copy<false, seg_u, true, DBL, kU, REC>), grid, s, a);
+    else if (direction == 0) launch((k_copy<true, seg_u, false, DBL, kU, REC>), grid, s, a);
+    else launch((k_copy<false, seg_u, false, DBL, kU, REC>), grid, s, a);
 }
 
 int launch_unstructured(const kargs& a, int direction, void* stream, uint32_t grid, bool runs)
 {
     if (a.n_tiles == 0) return GHX_OK;
+    grid = min(grid, a.n_tiles);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (a.parity_word)
     {
-        if (runs && direction == 0) launch((k_copy<true, seg_u, true, true>), grid, s, a);
-        else if (runs) launch((k_copy<false, seg_u, true, true>), grid, s, a);
-        else launch_u_general<true>(a, direction, s, grid);
+        if (a.tile_recs) launch_u<true, true>(a, direction, s, grid, runs);
+        else launch_u<true, false>(a, direction, s, grid, runs);
     }
-    else if (runs && direction == 0) launch((k_copy<true, seg_u, true>), grid, s, a);
-    else if (runs) launch((k_copy<false, seg_u, true>), grid, s, a);
-    else launch_u_general<false>(a, direction, s, grid);
+    else if (a.tile_recs) launch_u<false, true>(a, direction, s, grid, runs);
+    else launch_u<false, false>(a, direction, s, grid, runs);
     return launched("unstructured");
 }
 

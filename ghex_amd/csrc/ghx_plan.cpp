@@ -187,6 +187,21 @@ void upload(device_tables& dt, const std::vector<Seg>& segs, const std::vector<u
         throw hip_error("hipMemcpy(segments)");
     if (hipMemcpy(dt.tiles, tiles.data(), tb, hipMemcpyHostToDevice) != hipSuccess)
         throw hip_error("hipMemcpy(tiles)");
+    if (g_tune.tile_records && !tiles.empty())
+    {
+        // one record per tile, in dispatch order: the tile's segment with first_tile = the
+        // tile's index in it (a workgroup loads its record from blockIdx alone)
+        std::vector<Seg> rec(tiles.size() / 2);
+        for (size_t t = 0; t < rec.size(); ++t)
+        {
+            rec[t] = segs[tiles[2 * t]];
+            rec[t].first_tile = tiles[2 * t + 1];
+        }
+        const size_t rb = rec.size() * sizeof(Seg);
+        if (hipMalloc(&dt.recs, rb) != hipSuccess) throw hip_error("hipMalloc(tile records)");
+        if (hipMemcpy(dt.recs, rec.data(), rb, hipMemcpyHostToDevice) != hipSuccess)
+            throw hip_error("hipMemcpy(tile records)");
+    }
 }
 // Cut segments (in order) into launch groups of at most GHX_MAX_SLOTS distinct field and buffer
 // slots each; local[k] = segment k's slots inside its group. One group with identity maps
@@ -264,9 +279,11 @@ void device_tables::release()
 {
     if (segs) (void)hipFree(segs);
     if (tiles) (void)hipFree(tiles);
+    if (recs) (void)hipFree(recs);
     if (lids) (void)hipFree(lids);
     segs = nullptr;
     tiles = nullptr;
+    recs = nullptr;
     lids = nullptr;
 }
 
@@ -494,6 +511,7 @@ int splan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
         kargs a{};
         a.segs = dt.segs;
         a.tile_seg = dt.tiles;
+        a.tile_recs = dt.recs;
         a.n_tiles = nt;
         fill_slots(a.field_ptr, fptr, fm, max_field_slot + 1, "field");
         fill_slots(a.buf_ptr, bptr, bm, max_buf_slot + 1, "buffer");
@@ -725,6 +743,7 @@ int uplan::execute(void* const* fptr, int nf, void* const* bptr, int nb, void* s
         kargs a{};
         a.segs = dt.segs;
         a.tile_seg = dt.tiles;
+        a.tile_recs = dt.recs;
         a.n_tiles = nt;
         fill_slots(a.field_ptr, fptr, fm, max_field_slot + 1, "field");
         fill_slots(a.buf_ptr, bptr, bm, max_buf_slot + 1, "buffer");

@@ -23,6 +23,7 @@ struct device_tables
 {
     void* segs = nullptr;
     uint32_t* tiles = nullptr;
+    void* recs = nullptr;  // tile records (g_tune.tile_records): per tile a copy of its segment
     void* lids = nullptr;
     void release();
     device_tables() = default;

@@ -204,7 +204,7 @@ def test_read_floor_keys_say_floor_over_kernel():
     b = _bench()
 
     def probe(N, H, reps, us, c):
-        for i in range(8):
+        for i in range(10):
             us[i] = 10.0 + i
         for i in range(3):
             c[i] = 100 + i
@@ -218,6 +218,9 @@ def test_read_floor_keys_say_floor_over_kernel():
         b._floor_lib = orig
     assert out["floor_over_kernel"] == round(16.0 / 8.0, 3)
     assert out["write_floor"]["floor_over_kernel"] == round(16.0 / 32.0, 3)
+    # the unpack floor is the faster of the two buffer-read arrangements
+    assert out["write_floor"]["floor_us"] == 16.0
+    assert out["write_floor"]["writes_reads_interleaved_us"] == 18.0
     assert not any("vs_floor" in k for k in list(out) + list(out["write_floor"]))
     del ctypes
 
@@ -317,3 +320,56 @@ def test_cpu_baseline_config4_keys_and_parity_check():
     assert r["matches_gpu"] is True and r["value"] > 0
     buf[sb.fields[2].offset + 11] ^= 1
     assert bench.cpu_baseline_config4(0.01, buf)["matches_gpu"] is False
+
+
+def record_errors(o, path=""):
+    """Every key of a bench record that reports a failure ("error" or "*_error", non-empty),
+    with its path: a rehearsal leg that errored must never be summarised as verified (VERDICT
+    r05 #2). Skipped legs say "skipped", not "error"."""
+    out = []
+    if isinstance(o, dict):
+        for k, v in o.items():
+            p = f"{path}.{k}" if path else k
+            if (k == "error" or k.endswith("_error")) and v:
+                out.append((p, str(v)[:200]))
+            out += record_errors(v, p)
+    elif isinstance(o, list):
+        for i, v in enumerate(o):
+            out += record_errors(v, f"{path}[{i}]")
+    return out
+
+
+def _record_line(path):
+    import json
+    lines = [l for l in open(path) if l.startswith("{")]
+    assert lines, path
+    return json.loads(lines[-1])
+
+
+def test_record_errors_finds_nested_errors():
+    rec = {"value": 1, "bulk": {"isolated": True, "error": "exit 1: ghx_put_create failed"},
+           "extras": [{"transport_error": "x"}, {"skipped": "budget"}], "ok": {"error": ""}}
+    assert [p for p, _ in record_errors(rec)] == ["bulk.error", "extras[0].transport_error"]
+
+
+def test_latest_rehearsal_records_carry_no_error():
+    """The committed rehearsal records of the latest round (profiles/rNN*_rehearse_n*.json and
+    the isolated zero-copy legs rNN*_bulk_n*.json): no leg errored, and the zero-copy legs (puts
+    and the direct exchange) verified at N = 4 and 8 — the check that would have caught round
+    5's refused 512^3 put plans (profiles/r05h_rehearse_n4.json)."""
+    import glob
+    import re
+    files = glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_rehearse_n*.json")) + \
+        glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_bulk_n*.json"))
+    rnd = max(re.match(r"r(\d\d)", os.path.basename(f)).group(1) for f in files)
+    latest = [f for f in files if os.path.basename(f).startswith(f"r{rnd}")]
+    bulk_ok = set()
+    for f in latest:
+        rec = _record_line(f)
+        assert record_errors(rec) == [], (os.path.basename(f), record_errors(rec))
+        b = rec.get("bulk", rec if rec.get("mode") == "bulk-only" else None)
+        if b and b.get("verified") and b.get("direct", {}).get("verified"):
+            bulk_ok.add(rec.get("n_procs", rec.get("n_gpus")))
+    assert {4, 8} <= bulk_ok, (rnd, sorted(bulk_ok))
+    rec5 = _record_line(os.path.join(ROOT, "profiles", "r05h_rehearse_n4.json"))
+    assert [p for p, _ in record_errors(rec5)] == ["bulk.error"]  # the check sees round 5's

@@ -72,7 +72,7 @@ def main():
                 "pack_GBps": round(2 * n * 8 / kp / 1e9, 1),
                 "pack_floor_us": fl.get("reads_writes_us"),
                 "pack_floor_over_kernel": fl.get("floor_over_kernel"),
-                "unpack_floor_us": fl.get("write_floor", {}).get("writes_reads_us"),
+                "unpack_floor_us": fl.get("write_floor", {}).get("floor_us"),
                 "unpack_floor_over_kernel": fl.get("write_floor", {}).get("floor_over_kernel"),
                 "xface_lines": fl.get("xface_lines"), "xface_only_us": fl.get("xface_only_us")}),
                 flush=True)

@@ -88,6 +88,37 @@ __global__ __launch_bounds__(256) void k_pieces(const uint32_t* __restrict__ pie
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
 }
 
+// The unpack's mirror with the buffer reads interleaved with the writes, as the unpack kernel
+// issues them: per lane and step one list entry, the 16-B buffer vector of that position (the
+// buffer streamed lane-linearly) and the piece's store, kU steps in flight per lane. A piece of
+// 8 B takes a 16-B buffer slot (its second half unused): the stream is at most a few % longer
+// than the buffer.
+__global__ __launch_bounds__(256) void k_pieces_il(const uint32_t* __restrict__ pieces, uint32_t n,
+                                                   char* __restrict__ field,
+                                                   const v4* __restrict__ buf, unsigned* sink)
+{
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t base = blockIdx.x * 256u + threadIdx.x; base < n; base += kU * stride)
+    {
+        uint32_t q[kU];
+        v4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) q[u] = base + u * stride < n ? pieces[base + u * stride] : 0xffffffffu;
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (q[u] != 0xffffffffu) v[u] = buf[base + u * stride];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+        {
+            if (q[u] == 0xffffffffu) continue;
+            char* a = field + uint64_t(q[u] & 0x7fffffffu) * 8;
+            if (q[u] >> 31) *(v4*)a = v[u];
+            else *(unsigned __attribute__((ext_vector_type(2)))*)a = {v[u].x, v[u].y};
+        }
+    }
+    if (n == 0xffffffffu) sink[0] = 0;
+}
+
 // The fused self exchange's mirror: one grid loads one vector per pack line, streams the buffer
 // writes and writes every halo piece (what k_self must do, with no index arithmetic).
 __global__ __launch_bounds__(256) void k_fused(const uint32_t* __restrict__ lines, uint32_t nl,
@@ -185,8 +216,9 @@ static void piece_sets(int N, int H, std::vector<uint32_t>& xf, std::vector<uint
     std::sort(lg.begin(), lg.end(), [](uint32_t a, uint32_t b) { return (a & 0x7fffffffu) < (b & 0x7fffffffu); });
 }
 
-// out_us[8]: {xface, long, both, both + buffer reads} x {warm, cold} of the unpack's halo writes;
-// counts[3]: x-face pieces, long-row pieces, useful bytes. Returns 0, or the failing source line.
+// out_us[10]: {xface, long, both, both + buffer reads streamed first, both + buffer reads
+// interleaved (k_pieces_il)} x {warm, cold} of the unpack's halo writes; counts[3]: x-face pieces,
+// long-row pieces, useful bytes. Returns 0, or the failing source line.
 extern "C" int ghx_probe_unpack_floor(int N, int H, int reps, double* out_us, int64_t* counts)
 {
     int rc = 0;
@@ -209,7 +241,7 @@ extern "C" int ghx_probe_unpack_floor(int N, int H, int reps, double* out_us, in
     if (fbytes / 8 >= (size_t(1) << 31)) return __LINE__;  // piece addresses are 31-bit / 8
     CK(hipMalloc(&field, fbytes));
     CK(hipMalloc(&fl, flush_bytes));
-    CK(hipMalloc(&buf, useful + 64));
+    CK(hipMalloc(&buf, both.size() * 16 + 64));
     CK(hipMalloc(&sink, 64));
     CK(hipMalloc(&d_xf, xf.size() * 4 + 4));
     CK(hipMalloc(&d_lg, lg.size() * 4 + 4));
@@ -218,15 +250,15 @@ extern "C" int ghx_probe_unpack_floor(int N, int H, int reps, double* out_us, in
     CK(hipMemcpy(d_lg, lg.data(), lg.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_both, both.data(), both.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemset(field, 1, fbytes));
-    CK(hipMemset(buf, 3, useful + 64));
+    CK(hipMemset(buf, 3, both.size() * 16 + 64));
     CK(hipMemset(fl, 2, flush_bytes));
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     {
-        const uint32_t* lists[4] = {d_xf, d_lg, d_both, d_both};
-        const size_t ns[4] = {xf.size(), lg.size(), both.size(), both.size()};
-        const uint64_t rv[4] = {0, 0, 0, useful / 16};
-        for (int j = 0; j < 4; ++j)
+        const uint32_t* lists[5] = {d_xf, d_lg, d_both, d_both, d_both};
+        const size_t ns[5] = {xf.size(), lg.size(), both.size(), both.size(), both.size()};
+        const uint64_t rv[5] = {0, 0, 0, useful / 16, 0};
+        for (int j = 0; j < 5; ++j)
             for (int cold = 0; cold < 2; ++cold)
             {
                 std::vector<float> t;
@@ -235,11 +267,18 @@ extern "C" int ghx_probe_unpack_floor(int N, int H, int reps, double* out_us, in
                     if (cold)
                         hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, 0, (const v4*)fl,
                                            flush_bytes / 16, sink);
+                    else if (j == 4)
+                        hipLaunchKernelGGL(k_pieces_il, dim3(grid), dim3(256), 0, 0, lists[j],
+                                           uint32_t(ns[j]), field, (const v4*)buf, sink);
                     else
                         hipLaunchKernelGGL(k_pieces, dim3(grid), dim3(256), 0, 0, lists[j], uint32_t(ns[j]),
                                            field, (const v4*)buf, rv[j], sink);
-                    hipExtLaunchKernelGGL(k_pieces, dim3(grid), dim3(256), 0, 0, e0, e1, 0, lists[j],
-                                          uint32_t(ns[j]), field, (const v4*)buf, rv[j], sink);
+                    if (j == 4)
+                        hipExtLaunchKernelGGL(k_pieces_il, dim3(grid), dim3(256), 0, 0, e0, e1, 0,
+                                              lists[j], uint32_t(ns[j]), field, (const v4*)buf, sink);
+                    else
+                        hipExtLaunchKernelGGL(k_pieces, dim3(grid), dim3(256), 0, 0, e0, e1, 0, lists[j],
+                                              uint32_t(ns[j]), field, (const v4*)buf, rv[j], sink);
                     CK(hipEventSynchronize(e1));
                     float ms = 0;
                     CK(hipEventElapsedTime(&ms, e0, e1));
@@ -655,7 +694,7 @@ int main(int argc, char** argv)
 {
     const int reps = argc > 1 ? atoi(argv[1]) : 21;
     const int N = argc > 2 ? atoi(argv[2]) : 512, H = argc > 3 ? atoi(argv[3]) : 2;
-    double us[8];
+    double us[10];
     int64_t c[3];
     const int rc = ghx_probe_pack_floor(N, H, reps, us, c);
     if (rc)
@@ -677,8 +716,9 @@ int main(int argc, char** argv)
     }
     printf("{\"config\": \"%d^3 fp64 H=%d unpack write set\", \"useful_bytes\": %lld, \"xface_pieces\": %lld, "
            "\"long_pieces\": %lld}\n", N, H, (long long)c[2], (long long)c[0], (long long)c[1]);
-    const char* unames[4] = {"xface_writes", "long_writes", "writes", "writes_plus_buffer_reads"};
-    for (int j = 0; j < 4; ++j)
+    const char* unames[5] = {"xface_writes", "long_writes", "writes", "writes_plus_buffer_reads",
+                             "writes_buffer_reads_interleaved"};
+    for (int j = 0; j < 5; ++j)
         for (int cold = 0; cold < 2; ++cold)
             printf("{\"set\": \"%s\", \"cold\": %d, \"us\": %.2f}\n", unames[j], cold, us[2 * j + cold]);
     const int rc3 = ghx_probe_fused_floor(N, H, reps, us);

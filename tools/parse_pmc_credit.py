@@ -26,7 +26,10 @@ def summarise(d):
             if "tiles" not in r:
                 continue
             pack = cls.endswith("_pack")
-            c = s.get(f"k_copy<{'true' if pack else 'false'}, ghx::seg_s, false> wg={r['tiles']}")
+            # k_copy<PACK, seg_s, RUNS=false, ...> (round 6 added DBL / UU / REC parameters)
+            pre = f"k_copy<{'true' if pack else 'false'}, ghx::seg_s, false"
+            c = next((v for k, v in s.items()
+                      if k.startswith(pre) and k.endswith(f" wg={r['tiles']}")), None)
             if c:
                 raw[cls] = (r, c)
         base = raw["corner_pack"][1]["GRBM_GUI_ACTIVE"]
