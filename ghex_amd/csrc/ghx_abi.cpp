@@ -2,6 +2,7 @@
 // opaque handles, and the exchange planner (communication_object::allocate semantics).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstring>
 #include <list>
 #include <map>
@@ -1258,7 +1259,12 @@ int ghx_ipc_export(const void* ptr, unsigned char handle[64], uint64_t* offset)
             throw hip_error("hipMemGetAddressRange");
         hipIpcMemHandle_t h;
         if (hipIpcGetMemHandle(&h, reinterpret_cast<void*>(base)) != hipSuccess)
-            throw hip_error("hipIpcGetMemHandle");
+        {
+            char where[160];
+            std::snprintf(where, sizeof(where), "hipIpcGetMemHandle (ptr %p, allocation %p + %zu B)",
+                          ptr, reinterpret_cast<void*>(base), size);
+            throw hip_error(where);
+        }
         std::memcpy(handle, &h, sizeof(h));
         *offset = uint64_t(static_cast<const char*>(ptr) - reinterpret_cast<const char*>(base));
         return GHX_OK;

@@ -9,8 +9,18 @@ def device_field(a_mem: np.ndarray, layout, has_components=False):
     """a_mem is the numpy array in MEMORY order (slowest dim first, as helpers.* build them).
     Returns (base, logical): base = contiguous device copy in memory order, logical = a view of
     it indexed (x, y, z[, c]) whose strides realise `layout`."""
+    import os
+
     import torch
-    base = torch.from_numpy(np.ascontiguousarray(a_mem)).cuda()
+    how = os.environ.get("GHX_TEST_FIELD_ALLOC", "numpy")
+    host = torch.from_numpy(np.ascontiguousarray(a_mem))
+    if how == "pinned":  # H2D from page-locked host memory
+        base = host.pin_memory().cuda()
+    elif how == "device":  # allocated on the device first, then filled
+        base = torch.empty(host.shape, dtype=host.dtype, device="cuda")
+        base.copy_(host.pin_memory())
+    else:  # H2D from pageable host memory
+        base = host.cuda()
     nsp = len(layout) - (1 if has_components else 0)
     order = sorted(range(nsp), key=lambda d: layout[d])  # memory axis -> logical dim
     perm = [order.index(d) for d in range(nsp)]

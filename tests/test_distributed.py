@@ -240,3 +240,54 @@ def test_unstructured_multi_domain_ranks_gloo(golden_dir):
     with open(os.path.join(golden_dir, "unstructured_case.json")) as fh:
         case = json.load(fh)
     _run(2, _multi_domain_worker, case, [[0, 1], [2, 3]])
+
+
+def _certificate_worker(rank, world):
+    import types
+
+    import torch
+
+    import bench
+    plan = types.SimpleNamespace(
+        send=[{"rank": 1 - rank, "size": 100}, {"rank": rank, "size": 7},
+              {"rank": 1 - rank, "size": 20}],
+        recv=[{"rank": 1 - rank, "size": 60}, {"rank": rank, "size": 7}])
+    cert = bench.transport_certificate(torch, dist, torch.device("cuda", 0), plan, rank, world,
+                                       "gloo")
+    assert cert["world_size"] == 2 and cert["backend"] == "gloo" and cert["rccl_ranks"] is None
+    assert cert["devices"] == [0, 0]
+    peer = cert["peers"][str(1 - rank)]
+    assert peer["bytes_sent_per_step"] == 120 and peer["bytes_received_per_step"] == 60
+    assert peer.get("same_device") is True  # both ranks name device 0
+    assert cert["certified"] is False and "gloo" in cert["why_not"]
+    assert str(rank) not in cert["peers"]  # self messages are not a transport
+
+
+def test_transport_certificate_gloo_two_ranks():
+    """bench.transport_certificate over gloo on CPU: the world size and backend,
+    per-peer bytes from the plan's buffers (self messages excluded), and a line that is NOT
+    certified as an RCCL N-GPU run (gloo, shared device). The RCCL rank count is exercised by
+    the driver's N>1 runs."""
+    _run(2, _certificate_worker)
+
+
+def _collision_worker(rank, world):
+    import ghex_amd
+    from ghex_amd.unstructured import DomainDescriptor, HaloGenerator, make_pattern
+    ranks = [[(1, list(range(0, 10)), []), (2, list(range(10, 20)), [])],
+             [(8, list(range(20, 30)) + [10], [10]), (0, list(range(30, 40)) + [11], [10])]]
+    ctx = ghex_amd.make_context()
+    try:
+        make_pattern(ctx, HaloGenerator(), [DomainDescriptor(i, g, o) for i, g, o in ranks[rank]])
+    except Exception as e:
+        assert "share tag 8" in str(e), e
+        return
+    raise AssertionError("make_pattern returned despite a tag collision")
+
+
+def test_unstructured_setup_error_reaches_every_rank_gloo():
+    """a rank whose make_pattern<unstructured> fails mid-setup (here: a tag
+    collision found while resolving the reduced halos of the ring) must not leave its peers
+    waiting in the ring or a later collective; over gloo both ranks raise (the error names the
+    collision on the rank that saw it and on its peer)."""
+    _run(2, _collision_worker)

@@ -19,7 +19,8 @@
 // by its own begin/end events (hipExtLaunchKernelGGL: the interval a rocprofv3 kernel trace
 // reports, as bench.py's pack_kernel_us), median of `reps`.
 // Built by tools/Makefile (from __graft_entry__.build()) as tools/bin/pack_floor (one JSON line
-// per measurement) and tools/lib/libpackfloor.so (ghx_probe_pack_floor, called by bench.py).
+// per measurement; `pack_floor reps N H v` runs unpack variant v alone, warm, for the PMC passes
+// of tools/pmc_floor.sh) and tools/lib/libpackfloor.so (ghx_probe_pack_floor, called by bench.py).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -216,6 +217,9 @@ static void piece_sets(int N, int H, std::vector<uint32_t>& xf, std::vector<uint
     std::sort(lg.begin(), lg.end(), [](uint32_t a, uint32_t b) { return (a & 0x7fffffffu) < (b & 0x7fffffffu); });
 }
 
+// PMC runs (main's 4th argument): only this unpack variant, warm only (-1: all)
+static int s_only_variant = -1;
+
 // out_us[10]: {xface, long, both, both + buffer reads streamed first, both + buffer reads
 // interleaved (k_pieces_il)} x {warm, cold} of the unpack's halo writes; counts[3]: x-face pieces,
 // long-row pieces, useful bytes. Returns 0, or the failing source line.
@@ -261,6 +265,11 @@ extern "C" int ghx_probe_unpack_floor(int N, int H, int reps, double* out_us, in
         for (int j = 0; j < 5; ++j)
             for (int cold = 0; cold < 2; ++cold)
             {
+                if (s_only_variant >= 0 && (j != s_only_variant || cold))
+                {
+                    out_us[2 * j + cold] = 0;
+                    continue;
+                }
                 std::vector<float> t;
                 for (int i = 0; i < reps; ++i)
                 {
@@ -696,6 +705,15 @@ int main(int argc, char** argv)
     const int N = argc > 2 ? atoi(argv[2]) : 512, H = argc > 3 ? atoi(argv[3]) : 2;
     double us[10];
     int64_t c[3];
+    if (argc > 4)
+    {
+        // one unpack variant alone, warm (for rocprofv3 --pmc passes: tools/pmc_floor.sh)
+        s_only_variant = atoi(argv[4]);
+        const int rcv = ghx_probe_unpack_floor(N, H, reps, us, c);
+        printf("{\"unpack_variant\": %d, \"us\": %.2f, \"rc\": %d}\n", s_only_variant,
+               rcv ? -1.0 : us[2 * s_only_variant], rcv);
+        return rcv ? 1 : 0;
+    }
     const int rc = ghx_probe_pack_floor(N, H, reps, us, c);
     if (rc)
     {
