@@ -1304,8 +1304,9 @@ def pack_read_floor(N, Hw, roof):
     """The launches' address-set floors on this box (developer measurement, tools/pack_floor.hip
     via tools/lib/libpackfloor.so). Pack: a kernel that does nothing but load one
     16-B vector from each 128-B field line the pack must read (x-face lines first, as the pack
-    dispatches them) and stream the buffer writes. Unpack ("write_floor"): a kernel that streams
-    the buffer in and writes each halo row's bytes once (16-B pieces where aligned). Timed like
+    dispatches them) and stream the buffer writes. Unpack ("write_floor"): a kernel that writes
+    each halo row's bytes once (16-B pieces where aligned; floor_us), and the same with the
+    buffer read (streamed first / interleaved with the writes). Timed like
     pack_kernel_us (the kernel's own begin/end events, medians). floor_over_kernel = floor time /
     kernel time: above 1 the kernel is FASTER than its probe, below 1 slower."""
     import ctypes
@@ -1329,9 +1330,11 @@ def pack_read_floor(N, Hw, roof):
         if rc:
             out["write_floor"] = {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
         else:
-            # the floor: the faster of the two buffer-read arrangements (streamed first, or
-            # interleaved with the writes as the unpack kernel issues them)
-            fl = min(us[6], us[8])
+            # the floor: the halo pieces' writes alone (the unpack must issue them whatever it
+            # does with its buffer reads). The two probes that add the buffer reads (streamed
+            # first; interleaved with the writes, as the kernel issues them) are reported beside
+            # it: both are slower than the kernel, which overlaps its reads better
+            fl = us[4]
             out["write_floor"] = {
                 "xface_pieces": c[0], "long_pieces": c[1],
                 "xface_writes_us": round(us[0], 2), "long_writes_us": round(us[2], 2),

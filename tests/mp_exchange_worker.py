@@ -36,6 +36,20 @@ def make_jitter(rank):
     return jitter
 
 
+def _export_probe(tag, t):
+    """GHX_WORKER_EXPORT_PROBE=1: try ghx_ipc_export on `t` and print the outcome."""
+    import ctypes
+    import time
+
+    from ghex_amd import _ghx
+    L = _ghx.lib()
+    h = (ctypes.c_ubyte * 64)()
+    off = ctypes.c_uint64()
+    rc = L.ghx_ipc_export(ctypes.c_void_p(t.data_ptr()), h, ctypes.byref(off))
+    print(f"export_probe {tag} rc={rc} t={time.time():.3f} "
+          f"{L.ghx_last_error().decode()[:100] if rc else ''}", flush=True)
+
+
 def main():
     px, py, pz, N, Hw = (int(v) for v in sys.argv[1:6])
     reps = int(sys.argv[6]) if len(sys.argv) > 6 else 3
@@ -63,10 +77,21 @@ def main():
     dd = R.DomainDescriptor(dom.id, dom.first, dom.last)
     pc = R.make_pattern(ctx, R.HaloGenerator(gf, gl, (Hw,) * 6, (True,) * 3), [dd])
     bad = 0
+    probe = os.environ.get("GHX_WORKER_EXPORT_PROBE") == "1"  # developer diagnosis
+    if probe:
+        _export_probe("start", torch.empty((N + 2 * Hw,) * 3, dtype=torch.float64, device="cuda"))
     for layout in [(2, 1, 0), (0, 2, 1)]:
         a, _ = H.linear_index_field(dom, N, Hw, gl, layout=layout)
+        if probe:
+            _export_probe("after_field_numpy", torch.empty(a.shape, dtype=torch.float64,
+                                                           device="cuda"))
         expect = H.expected_linear_halo(a, dom, N, Hw, gl, layout=layout)
+        if probe:
+            _export_probe("after_expect_numpy", torch.empty(a.shape, dtype=torch.float64,
+                                                            device="cuda"))
         base, logical = device_field(a, layout)
+        if probe:
+            _export_probe("field", base)
         fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)
         if mode in ("bulk", "bulkhost"):
             co = ghex_amd.make_bulk_communication_object(

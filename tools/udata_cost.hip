@@ -3,7 +3,10 @@
 // &stream), at BASELINE config 5's list size (one neighbour list of `n_lids` random lids into a
 // 10.5M-cell fp64 field, levels 1), against the device time of the gather it enqueues.
 //
-//   adaptor   data_descriptor::pack (plan found by the list's address: O(1) host work)
+//   adaptor   data_descriptor::pack (plan found by the list's address, the list compared with
+//             the plan's copy in full: the default since round 6)
+//   adaptor_sampled   the same with assume_immutable_index_lists(true) (16 sampled entries:
+//             O(1) host work; round 5's default)
 //   c_entry   ghx_unstructured_pack (the plain C entry point: compares the whole list with the
 //             cached copy on every call — what the adaptor called before round 5)
 //   launch    ghx_uplan_execute of a prepared plan (the launch alone: the floor of any call)
@@ -101,6 +104,9 @@ int main(int argc, char** argv)
     ghex_amd::unstructured::data_descriptor<int, double> d(0, size_t(cells), values, 1, true);
     const auto& l = c[0].local_indices();
     auto adaptor = [&] { d.pack(buf, c, &s); };
+    ghex_amd::unstructured::data_descriptor<int, double> d2(0, size_t(cells), values, 1, true);
+    d2.assume_immutable_index_lists(true);
+    auto sampled = [&] { d2.pack(buf, c, &s); };
     auto c_entry = [&] {
         ghex_amd::unstructured::check_u(
             ghx_unstructured_pack(&d.desc(), values, buf, l.data(), 4, int64_t(l.size()), s),
@@ -119,22 +125,24 @@ int main(int argc, char** argv)
     for (int i = 0; i < 20; ++i)
     {
         adaptor();
+        sampled();
         c_entry();
         launch();
     }
     HCK(hipStreamSynchronize(s));
     const int reps = 200;
     const double h_ad = host_us(s, adaptor, reps), h_c = host_us(s, c_entry, reps),
-                 h_l = host_us(s, launch, reps);
+                 h_l = host_us(s, launch, reps), h_sm = host_us(s, sampled, reps);
     const double d_ad = device_us(s, adaptor, 100), d_c = device_us(s, c_entry, 100),
-                 d_l = device_us(s, launch, 100);
+                 d_l = device_us(s, launch, 100), d_sm = device_us(s, sampled, 100);
     std::printf("{\"n_lids\": %lld, \"cells\": %lld, \"levels\": 1, "
                 "\"adaptor\": {\"host_us\": %.3f, \"device_us\": %.3f}, "
+                "\"adaptor_sampled\": {\"host_us\": %.3f, \"device_us\": %.3f}, "
                 "\"c_entry\": {\"host_us\": %.3f, \"device_us\": %.3f}, "
                 "\"launch\": {\"host_us\": %.3f, \"device_us\": %.3f}, "
                 "\"adaptor_overhead_us\": %.3f, \"adaptor_overhead_frac_of_device\": %.4f, "
                 "\"c_entry_overhead_us\": %.3f, \"c_entry_overhead_frac_of_device\": %.4f}\n",
-                (long long)n_lids, (long long)cells, h_ad, d_ad, h_c, d_c, h_l, d_l, h_ad - h_l,
+                (long long)n_lids, (long long)cells, h_ad, d_ad, h_sm, d_sm, h_c, d_c, h_l, d_l, h_ad - h_l,
                 (h_ad - h_l) / d_l, h_c - h_l, (h_c - h_l) / d_l);
     ghx_uplan_destroy(p);
     HCK(hipFree(values));
