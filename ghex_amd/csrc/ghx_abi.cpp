@@ -267,7 +267,9 @@ struct ghx_put
                                "message bytes (shapes, order, element sizes or row structure differ)");
         if (from->grouped() || to->grouped())
             throw ghx::invalid("a put plan takes at most 64 source and 64 target fields (one launch)");
+        ghx::upload_pair_records(recs, from->host_segs, to->host_segs, from->host_tiles);
     }
+    ghx::device_tables recs;  // pair records (source segment with tile index, target segment)
 };
 
 using namespace ghx;
@@ -460,6 +462,7 @@ void build_mixed(exchange_plan& ex, int32_t me, const std::vector<ghx_pack_entry
     // (tools/emu_rank_bench.py, profiles/r01c_emu_rank.jsonl).
     if (!short_self && !g_tune.mixed_always) return;
     upload_segments(ex.mixed_comp, comp);
+    upload_pair_records(ex.mixed_recs, ps, comp, ex.spack->host_tiles);
     ex.mixed_max_field_slot = su.max_field_slot;
     ex.punpack = std::make_unique<splan>(peer_e.data(), int(peer_e.size()), 1);
     ex.mixed = true;
@@ -1009,6 +1012,12 @@ int ghx_exchange_create(const ghx_exchange_item* items, int32_t n_items, ghx_exc
             ex->self_pack.reset();
             ex->self_unpack.reset();
         }
+        if (ex->self_fusable())
+        {
+            const splan& p = ex->self_pack ? *ex->self_pack : *ex->spack;
+            const splan& q = ex->self_unpack ? *ex->self_unpack : *ex->sunpack;
+            upload_pair_records(ex->self_recs, p.host_segs, q.host_segs, p.host_tiles);
+        }
         build_mixed(*ex, items[0].pattern->my_rank, rent);
         *out = ex.release();
         return GHX_OK;
@@ -1137,6 +1146,7 @@ int ghx_exchange_self(const ghx_exchange* ex, void* const* field_ptrs, int32_t n
         a.segs = p.dev.segs;
         a.segs2 = q.dev.segs;
         a.tile_seg = p.dev.tiles;
+        a.tile_recs = ex->self_recs.recs;
         a.n_tiles = p.n_tiles;
         for (int i = 0; i <= nfs; ++i)
         {
@@ -1179,6 +1189,7 @@ int ghx_exchange_pack_self(const ghx_exchange* ex, void* const* field_ptrs, int3
         a.segs = p.dev.segs;
         a.segs2 = ex->mixed_comp.segs;
         a.tile_seg = p.dev.tiles;
+        a.tile_recs = ex->mixed_recs.recs;
         a.n_tiles = p.n_tiles;
         for (int i = 0; i <= nfs; ++i)
         {
@@ -1325,6 +1336,7 @@ int ghx_put_execute(const ghx_put* put, void* const* src_fields, int32_t n_src,
         a.segs = p.dev.segs;
         a.segs2 = q.dev.segs;
         a.tile_seg = p.dev.tiles;
+        a.tile_recs = put->recs.recs;
         a.n_tiles = p.n_tiles;
         for (int i = 0; i <= p.max_field_slot; ++i)
         {

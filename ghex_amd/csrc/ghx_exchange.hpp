@@ -28,6 +28,9 @@ struct exchange_plan
     // segment of its self message (zero = a peer message: pack only), and the unpack plan of
     // the peer messages alone
     device_tables mixed_comp;
+    // pair records of the fused launches (upload_pair_records): the all-self exchange's
+    // (ghx_exchange_self) and the mixed pack's (ghx_exchange_pack_self); empty: tile table path
+    device_tables self_recs, mixed_recs;
     int mixed_max_field_slot = -1;  // the highest field slot mixed_comp's segments name
     std::unique_ptr<splan> punpack;
     bool mixed = false;
@@ -100,7 +103,7 @@ struct exchange_plan
     }
 
     // Every recv buffer aliases the send buffer of the same pair, and pack segment k and unpack
-    // segment k cover the same buffer bytes with the same tiling.
+    // segment k cover the same buffer bytes (the launch tiles by the pack plan's table).
     bool self_fusable() const
     {
         if (self_ok >= 0) return self_ok == 1;

@@ -626,19 +626,33 @@ __device__ __forceinline__ void self_forward(const seg_s& s, const seg_s& q,
 // it writes the halo from the registers it stored the buffer from (self_forward), no barrier.
 // Otherwise the workgroup packs its tile (field interior -> buffer), passes a workgroup barrier
 // (its own stores are visible to its own waves), then unpacks the same bytes (buffer -> halo).
-template<bool DBL = false>
+// REC: pair records (upload_pair_records) — the workgroup loads its tile's pack and unpack
+// segments side by side at tile_recs[2 * blockIdx.x], no tile-table load ahead of them.
+template<bool DBL = false, bool REC = false>
 __global__ __launch_bounds__(kBlock) void k_self(kargs a)
 {
     const seg_s* __restrict__ ps = static_cast<const seg_s*>(a.segs);
     const seg_s* __restrict__ us = static_cast<const seg_s*>(a.segs2);
+    const seg_s* __restrict__ rec = static_cast<const seg_s*>(a.tile_recs);
     bool odd = false;
     if constexpr (DBL) odd = odd_parity(a);
     for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
     {
-        const uint32_t si = a.tile_seg[2 * t];
-        const uint32_t ti = a.tile_seg[2 * t + 1];
-        const seg_s s = ps[si];
-        const seg_s q = us[si];
+        seg_s s, q;
+        uint32_t ti;
+        if constexpr (REC)
+        {
+            s = rec[2 * t];
+            q = rec[2 * t + 1];
+            ti = s.first_tile;
+        }
+        else
+        {
+            const uint32_t si = a.tile_seg[2 * t];
+            ti = a.tile_seg[2 * t + 1];
+            s = ps[si];
+            q = us[si];
+        }
         const uint32_t start = ti * s.tile_bytes;
         const uint32_t end = min(start + s.tile_bytes, s.bytes);
         char* field_p = reinterpret_cast<char*>(a.field_ptr[s.field_slot]);
@@ -707,16 +721,29 @@ __device__ __forceinline__ void copy_direct(const seg_s& s, const seg_s& q,
     }
 }
 
+template<bool REC = false>
 __global__ __launch_bounds__(kBlock) void k_put(kargs a)
 {
     const seg_s* __restrict__ ps = static_cast<const seg_s*>(a.segs);
     const seg_s* __restrict__ qs = static_cast<const seg_s*>(a.segs2);
+    const seg_s* __restrict__ rec = static_cast<const seg_s*>(a.tile_recs);
     for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x)
     {
-        const uint32_t si = a.tile_seg[2 * t];
-        const uint32_t ti = a.tile_seg[2 * t + 1];
-        const seg_s s = ps[si];
-        const seg_s q = qs[si];
+        seg_s s, q;
+        uint32_t ti;
+        if constexpr (REC)
+        {
+            s = rec[2 * t];
+            q = rec[2 * t + 1];
+            ti = s.first_tile;
+        }
+        else
+        {
+            const uint32_t si = a.tile_seg[2 * t];
+            ti = a.tile_seg[2 * t + 1];
+            s = ps[si];
+            q = qs[si];
+        }
         const uint32_t start = ti * s.tile_bytes;
         const uint32_t end = min(start + s.tile_bytes, s.bytes);
         const char* src = reinterpret_cast<const char*>(a.field_ptr[s.field_slot]);
@@ -822,15 +849,22 @@ int launch_structured(const kargs& a, int direction, void* stream, uint32_t grid
 int launch_self(const kargs& a, void* stream, uint32_t grid)
 {
     if (a.n_tiles == 0) return GHX_OK;
-    if (a.parity_word) launch(k_self<true>, grid, static_cast<hipStream_t>(stream), a);
-    else launch(k_self<false>, grid, static_cast<hipStream_t>(stream), a);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (a.parity_word)
+    {
+        if (a.tile_recs) launch((k_self<true, true>), grid, s, a);
+        else launch((k_self<true, false>), grid, s, a);
+    }
+    else if (a.tile_recs) launch((k_self<false, true>), grid, s, a);
+    else launch((k_self<false, false>), grid, s, a);
     return launched("self-exchange");
 }
 
 int launch_put(const kargs& a, void* stream, uint32_t grid)
 {
     if (a.n_tiles == 0) return GHX_OK;
-    launch(k_put, grid, static_cast<hipStream_t>(stream), a);
+    if (a.tile_recs) launch(k_put<true>, grid, static_cast<hipStream_t>(stream), a);
+    else launch(k_put<false>, grid, static_cast<hipStream_t>(stream), a);
     return launched("put");
 }
 

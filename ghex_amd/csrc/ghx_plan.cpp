@@ -297,6 +297,26 @@ void upload_segments(device_tables& dt, const std::vector<seg_s>& segs)
         throw hip_error("hipMemcpy(segments)");
 }
 
+void upload_pair_records(device_tables& dt, const std::vector<seg_s>& primary,
+                         const std::vector<seg_s>& companion, const std::vector<uint32_t>& tiles)
+{
+    dt.release();
+    if (!g_tune.tile_records || tiles.empty() || !have_device()) return;
+    if (primary.size() != companion.size()) throw invalid("pair records: segment counts differ");
+    std::vector<seg_s> rec(tiles.size());  // 2 per tile
+    for (size_t t = 0; t < tiles.size() / 2; ++t)
+    {
+        const uint32_t si = tiles[2 * t];
+        rec[2 * t] = primary[si];
+        rec[2 * t].first_tile = tiles[2 * t + 1];
+        rec[2 * t + 1] = companion[si];
+    }
+    const size_t rb = rec.size() * sizeof(seg_s);
+    if (hipMalloc(&dt.recs, rb) != hipSuccess) throw hip_error("hipMalloc(pair records)");
+    if (hipMemcpy(dt.recs, rec.data(), rb, hipMemcpyHostToDevice) != hipSuccess)
+        throw hip_error("hipMemcpy(pair records)");
+}
+
 // ---------------------------------------------------------------------------------------------
 // structured
 // ---------------------------------------------------------------------------------------------
@@ -478,6 +498,7 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
         {
             n_tiles = uint32_t(tiles.size() / 2);
             host_segs = gs;
+            host_tiles = tiles;
             fmap = part.fmap[0];
             bmap = part.bmap[0];
             upload(dev, gs, tiles);

@@ -35,6 +35,12 @@ struct device_tables
 void validate_field(const ghx_field_desc& f);
 // segment table alone to device memory (a no-op without a HIP device)
 void upload_segments(device_tables& dt, const std::vector<seg_s>& segs);
+// Pair records of a fused launch (k_self, k_put; g_tune.tile_records): per tile of the primary
+// plan, in its dispatch order, the primary segment (with the tile's index in first_tile) and
+// the companion segment of the same index, side by side (dt.recs; a no-op without a device or
+// with tile_records off)
+void upload_pair_records(device_tables& dt, const std::vector<seg_s>& primary,
+                         const std::vector<seg_s>& companion, const std::vector<uint32_t>& tiles);
 uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, const ghx_box& box,
                           uint16_t field_slot, uint16_t buf_slot, uint64_t buf_off);
 
@@ -63,6 +69,7 @@ struct splan
     uint32_t tile_bytes = kTileBytes;
     int max_field_slot = -1, max_buf_slot = -1;  // caller slots
     std::vector<seg_s> host_segs;                // the first group's, local slots
+    std::vector<uint32_t> host_tiles;            // the first group's tile table (pair records)
     device_tables dev;
     std::vector<int32_t> fmap, bmap;             // the first group's slot maps (empty: identity)
     std::vector<std::unique_ptr<slot_group<seg_s>>> more;  // further launch groups

@@ -106,11 +106,13 @@ def fused_vs_unfused(Hw, layout, N):
 @pytest.mark.parametrize("knobs", [{"self_tile_bytes": 8192}, {"self_tile_bytes": 4096},
                                    {"self_tile_bytes": 2048, "grid_cap": 5},
                                    {"self_tile_bytes": 65536, "xcd_pair": 0},
-                                   {"short_pol": 3}])
+                                   {"short_pol": 3}, {"tile_records": 0},
+                                   {"self_tile_bytes": 4096, "tile_records": 0, "grid_cap": 5}])
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_self_kernel_variants_stay_bit_exact(knobs, Hw):
     """The fused self kernel under its remaining knobs (tile sizes, a grid-stride loop, XCD
-    pairing off, cache policies) writes the oracle's buffer bytes and halos."""
+    pairing off, cache policies, the tile-table path instead of pair records) writes the
+    oracle's buffer bytes and halos."""
     from ghex_amd import _ghx
     try:
         for k, v in knobs.items():

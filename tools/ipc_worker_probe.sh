@@ -14,14 +14,14 @@ step_world() {  # name px py pz N mode
   local pids=()
   for ((r = 0; r < w; r++)); do
     env RANK=$r WORLD_SIZE=$w MASTER_ADDR=127.0.0.1 MASTER_PORT=$port LOCAL_RANK=0 AMD_LOG_LEVEL=1 \
-      GHX_TEST_FIELD_ALLOC=${ALLOC:-numpy} \
+      GHX_TEST_FIELD_ALLOC=${ALLOC:-numpy} GHX_WORKER_EXPORT_PROBE=${PROBE:-0} \
       timeout -k 10 150 python tests/mp_exchange_worker.py $1 $2 $3 $4 2 1 $5 > $OUT/${name}_r$r.log 2>&1 &
     pids+=($!)
   done
   local worst=0
   for p in "${pids[@]}"; do wait $p; rc=$?; [ $rc -gt $worst ] && worst=$rc; done
   echo "$name rc=$worst $(grep -h 'bad cells' $OUT/${name}_r0.log)" >> $OUT/status
-  grep -h "hipIpcGetMemHandle\|IPC memory creation" $OUT/${name}_r*.log | head -8 >> $OUT/status
+  grep -h "hipIpcGetMemHandle\|IPC memory creation\|export_probe" $OUT/${name}_r*.log | head -24 >> $OUT/status
   if [ $worst -gt 1 ]; then exit $worst; fi
 }
 for a in ${ALLOCS:-numpy}; do

@@ -13,6 +13,7 @@ GROUPS_=("TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACT
          "TCC_EA0_WRREQ_LEVEL_sum TCC_EA0_RDREQ_LEVEL_sum GRBM_GUI_ACTIVE")
 for v in 2 3 4; do
   i=0
+  mkdir -p $OUT/v$v
   for grp in "${GROUPS_[@]}"; do
     i=$((i+1))
     timeout -s KILL 60 rocprofv3 --pmc $grp --kernel-trace -d $OUT/v$v/p$i -o pmc --output-format csv -- $R/tools/bin/pack_floor 7 $N $H $v > $OUT/v$v/p$i.log 2>&1 || { echo "pmc v$v p$i failed" >> $OUT/status; exit 1; }
