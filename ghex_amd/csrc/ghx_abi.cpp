@@ -504,6 +504,12 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 1) throw invalid("mixed_always must be 0 or 1");
             g_tune.mixed_always = value;
         }
+        else if (k == "unpack_tile_bytes")
+        {
+            if (value != 0 && (value < 1024 || uint32_t(value) > kMaxTileBytes || (value & (value - 1))))
+                throw invalid("unpack_tile_bytes must be 0 or a power of two in [1 KiB, 1 MiB]");
+            g_tune.unpack_tile_bytes = uint32_t(value);
+        }
         else if (k == "tile_records")
         {
             if (value < 0 || value > 1) throw invalid("tile_records must be 0 or 1");

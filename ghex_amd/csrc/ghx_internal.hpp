@@ -30,6 +30,8 @@ struct tuning
 {
     int grid_cap = 0;               // >0: at most this many workgroups (grid-stride beyond)
     uint32_t tile_bytes = kTileBytes;  // tile of segments with long rows
+    uint32_t unpack_tile_bytes = 0;    // the same for unpack plans (0: tile_bytes); above 8 KiB
+                                       // the unpack kernel pipelines a tile's steps
     uint32_t self_tile_bytes = kTileBytes;  // the same for the fused self exchange (separate
                                        // self plans are built when it differs). Medians of 4
                                        // interleaved A/B runs with register forwarding:
@@ -102,7 +104,7 @@ struct alignas(16) seg_s
     uint8_t wlog2;        // log2 of the widest vector (<= 16 B) that divides L, offsets, strides
     uint8_t n_outer;
     uint8_t fpol;         // field-side cache policy: bit 0 nt loads, bit 1 sc1 stores
-    uint8_t pad1;
+    uint8_t pipe;         // unpack of long rows in tiles of several steps: software-pipelined
     uint32_t tile_bytes;  // this segment's tile size (a multiple of the row length or 16 KiB)
     uint8_t pad[8];
 };

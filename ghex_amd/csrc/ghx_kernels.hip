@@ -220,6 +220,65 @@ __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field
     }
 }
 
+// The unpack of a tile of several steps (unpack plans with long-row tiles above 8 KiB,
+// g_tune.unpack_tile_bytes), software-pipelined: each lane issues the buffer loads of step k+1
+// before the field stores of step k, so a workgroup keeps its reads in flight while its writes
+// drain (the unpack is bound by its writes, §4.4 of DESIGN.md); kP vectors per lane per step.
+template<int W, typename Seg>
+__device__ __forceinline__ void unpack_tile_pipelined(const Seg& s, char* __restrict__ field,
+                                                      char* __restrict__ buf, uint32_t start,
+                                                      uint32_t end)
+{
+    using V = typename vec_t<W>::type;
+    constexpr int kP = 2;
+    const uint32_t pol = s.fpol;
+    const uint32_t step = kP * kBlock * W;
+    uint32_t base = start + threadIdx.x * W;
+    if (base >= end) return;
+    V v[kP];
+    int64_t fo[kP];
+#pragma unroll
+    for (int u = 0; u < kP; ++u)
+    {
+        const uint32_t p = base + u * kBlock * W;
+        if (p < end)
+        {
+            fo[u] = field_offset<Seg>(s, p);
+            v[u] = vload<V>(buf + p);
+        }
+    }
+    for (;;)
+    {
+        const uint32_t nb = base + step;
+        const bool more = nb < end;
+        V w[kP];
+        int64_t fn[kP];
+        if (more)
+        {
+#pragma unroll
+            for (int u = 0; u < kP; ++u)
+            {
+                const uint32_t p = nb + u * kBlock * W;
+                if (p < end)
+                {
+                    fn[u] = field_offset<Seg>(s, p);
+                    w[u] = vload<V>(buf + p);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kP; ++u)
+            if (base + u * kBlock * W < end) fstore<V>(field + fo[u], v[u], pol);
+        if (!more) break;
+        base = nb;
+        for (int u = 0; u < kP; ++u)  // register renaming (fully unrolled by the compiler)
+        {
+            v[u] = w[u];
+            fo[u] = fn[u];
+        }
+    }
+}
+
 // Unstructured rows of L = 4 or 8 bytes with run detection (seg_u::runs): lane t of a wave moves
 // the 16-B buffer chunk [p, p+16) = rows r0 .. r0+K-1 (K = 16/L). It loads the chunk's K lids
 // with one vector load and tests whether they form a run (lid[j] = lid[0] + j): then the K rows
@@ -504,6 +563,12 @@ template<bool PACK, int UU, typename Seg>
 __device__ __forceinline__ void copy_any(const Seg& s, char* field, char* buf, uint32_t start,
                                          uint32_t end, int w)
 {
+    if constexpr (!PACK)
+        if (s.pipe && w == 4)  // long rows in tiles of several steps (planner: unpack_tile_bytes)
+        {
+            unpack_tile_pipelined<16>(s, field, buf, start, end);
+            return;
+        }
     switch (w)
     {
         case 4: copy_tile<PACK, 16>(s, field, buf, start, end); break;

@@ -84,19 +84,25 @@ uint32_t short_tile_rows(const seg_u& s, uint64_t)
     return s.runs == 2 ? g_tune.u_run_tile_rows : g_tune.u_tile_rows;
 }
 // tile of segments with long rows: structured / unstructured
-uint32_t long_tile_bytes(const seg_s&) { return g_tune.tile_bytes; }
-uint32_t long_tile_bytes(const seg_u& s)
+uint32_t long_tile_bytes(const seg_s&, int dir)
+{
+    return dir == 1 && g_tune.unpack_tile_bytes ? g_tune.unpack_tile_bytes : g_tune.tile_bytes;
+}
+uint32_t long_tile_bytes(const seg_u& s, int)
 {
     // whole rows per tile (at least one)
     const uint32_t tb = std::max<uint32_t>(g_tune.u_tile_bytes, s.row_bytes);
     return tb - tb % s.row_bytes;
 }
 
+void set_pipe(seg_s& s, bool on) { s.pipe = on ? 1 : 0; }
+void set_pipe(seg_u&, bool) {}
+
 // Tile table: per tile {segment, tile index within the segment}. Segments with short rows
 // (request-bound: one memory request per row) may use a different tile size from streaming
 // segments; the dispatch order of tiles is a tuning knob (hardware dispatches in blockIdx order).
 template<typename Seg>
-std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
+std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, int dir)
 {
     std::vector<std::vector<uint32_t>> per(segs.size());
     // each field's short rows (its request-bound work): a field's short-row tiles are sized by
@@ -109,7 +115,7 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
     for (uint32_t i = 0; i < segs.size(); ++i)
     {
         const bool small = segs[i].row_bytes < g_tune.small_row_bytes;
-        uint32_t tb = long_tile_bytes(segs[i]);
+        uint32_t tb = long_tile_bytes(segs[i], dir);
         if (small)
         {
             const uint32_t rows = short_tile_rows(segs[i], short_rows[segs[i].field_slot]);
@@ -119,6 +125,7 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs)
         }
         segs[i].tile_bytes = tb;
         segs[i].fpol = small ? uint8_t(g_tune.short_pol) : uint8_t(0);
+        set_pipe(segs[i], !small && dir == 1 && g_tune.unpack_tile_bytes > kTileBytes);
         segs[i].first_tile = 0;
         const uint32_t nt = tiles_of(segs[i].bytes, tb);
         for (uint32_t t = 0; t < nt; ++t) per[i].push_back(t);
@@ -493,7 +500,7 @@ splan::splan(const ghx_pack_entry* entries, int n_entries, int dir) : direction(
             x.buf_slot = uint16_t(part.lb[k]);
             gs.push_back(x);
         }
-        std::vector<uint32_t> tiles = build_tiles(gs);
+        std::vector<uint32_t> tiles = build_tiles(gs, direction);
         if (g == 0)
         {
             n_tiles = uint32_t(tiles.size() / 2);
@@ -723,7 +730,7 @@ uplan::uplan(const ghx_upack_entry* entries, int n_entries, int dir) : direction
             x.buf_slot = uint16_t(part.lb[k]);
             gs.push_back(x);
         }
-        std::vector<uint32_t> tiles = build_tiles(gs);
+        std::vector<uint32_t> tiles = build_tiles(gs, direction);
         if (g == 0)
         {
             n_tiles = uint32_t(tiles.size() / 2);

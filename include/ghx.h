@@ -56,7 +56,9 @@ typedef void* ghx_stream;
  * for 4/8-B index-list rows), "u_run_tile_rows" (rows per tile of run-heavy index lists), "self_tile_bytes" (tile of the fused self exchange),
  * "mixed_always" (0|1: build mixed self/peer plans even without short-row self messages),
  * "tile_records" (0|1: the pack / unpack launches read one per-tile record addressed by the
- * workgroup index instead of a tile table entry and then its segment; default 1);
+ * workgroup index instead of a tile table entry and then its segment; default 1),
+ * "unpack_tile_bytes" (0 = tile_bytes, the default; else the long-row tile of unpack plans, whose
+ * tiles of several steps the unpack kernel then software-pipelines);
  * "reset" restores every default. Plan-shaping knobs apply to plans created afterwards. Unknown
  * keys fail with GHX_ERR_INVALID (the variants removed in round 3 are listed in
  * tools/kernel_variants_r02.hip).

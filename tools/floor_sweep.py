@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="")
     ap.add_argument("--tune", action="append", default=[])
+    ap.add_argument("--no-floor", action="store_true", help="kernels only (no probes)")
     a = ap.parse_args()
     shapes = [tuple(int(x) for x in sh.split(":")) for sh in a.shapes.split(",") if sh] or \
         [(N, H) for N in (256, 384, 512, 640) for H in (1, 2, 3)]
@@ -64,7 +65,7 @@ def main():
             want = (idx.view(1, 1, E) + N * (idx.view(1, E, 1) + N * idx.view(E, 1, 1))).double()
             ok = bool((f == want).all())
             roof = {"pack_kernel_us": round(kp * 1e6, 2), "unpack_kernel_us": round(ku * 1e6, 2)}
-            fl = bench.pack_read_floor(N, H, roof)
+            fl = {} if a.no_floor else bench.pack_read_floor(N, H, roof)
             n = E ** 3 - N ** 3
             print(json.dumps({
                 "tune": st, "N": N, "H": H, "row_pitch_bytes": E * 8, "verified": ok,
