@@ -515,6 +515,11 @@ int ghx_tune(const char* key, int32_t value)
             if (value < 0 || value > 1) throw invalid("tile_records must be 0 or 1");
             g_tune.tile_records = value;
         }
+        else if (k == "fast_addr")
+        {
+            if (value < 0 || value > 1) throw invalid("fast_addr must be 0 or 1");
+            g_tune.fast_addr = value;
+        }
         else if (k == "xcd_pair")
         {
             if (value < 0 || value > 1) throw invalid("xcd_pair must be 0 or 1");

@@ -61,6 +61,9 @@ struct tuning
     int tile_records = 1;              // k_copy reads per tile ONE record (its segment with the
                                        // tile index in first_tile) at blockIdx: no dependent
                                        // tile-table load ahead of the segment load
+    int fast_addr = 1;                 // structured segments whose offsets fit the short form
+                                       // (seg_s::amode) decode rows with 1-2 divisions and
+                                       // full-rate 24-bit products instead of int64 ones
 };
 extern tuning g_tune;
 
@@ -106,7 +109,10 @@ struct alignas(16) seg_s
     uint8_t fpol;         // field-side cache policy: bit 0 nt loads, bit 1 sc1 stores
     uint8_t pipe;         // unpack of long rows in tiles of several steps: software-pipelined
     uint32_t tile_bytes;  // this segment's tile size (a multiple of the row length or 16 KiB)
-    uint8_t pad[8];
+    uint8_t amode;        // field-offset arithmetic (planner, set_amode): 0 general (int64, 3
+                          // divisions), 1 / 2: 32-bit offsets relative to field_off from 24-bit
+                          // products, 1 / 2 divisions (n_outer <= 2 / == 3), see field_offset_f
+    uint8_t pad[7];
 };
 static_assert(sizeof(seg_s) == 128, "seg_s layout");
 

@@ -21,6 +21,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -164,6 +165,28 @@ __device__ __forceinline__ int64_t field_offset_s(const seg_s& s, uint32_t p)
            int64_t(c2) * s.stride[2] + int64_t(q2) * s.stride[3] + int64_t(col);
 }
 
+// The short form (seg_s::amode 1 / 2, planner short_addressing): the offset of buffer position
+// p RELATIVE to s.field_off, in 32 bits. Every product has both operands below 2^24 and a result
+// below 2^32, so the full-rate v_mul_u32_u24 is exact; the last outer coordinate is the quotient
+// itself (rows < ext[0]*ext[1](*ext[2])), so NDIV = n_outer - 1 divisions (at least one).
+template<int NDIV>
+__device__ __forceinline__ uint32_t field_offset_f(const seg_s& s, uint32_t p)
+{
+    const uint32_t row = fastdiv(p, s.mag_row);
+    uint32_t off = p - __umul24(row, s.row_bytes);
+    const uint32_t q0 = fastdiv(row, s.mag_ext[0]);
+    off += __umul24(row - __umul24(q0, s.ext[0]), uint32_t(s.stride[0]));
+    if constexpr (NDIV == 1)
+        off += __umul24(q0, uint32_t(s.stride[1]));
+    else
+    {
+        const uint32_t q1 = fastdiv(q0, s.mag_ext[1]);
+        off += __umul24(q0 - __umul24(q1, s.ext[1]), uint32_t(s.stride[1]));
+        off += __umul24(q1, uint32_t(s.stride[2]));
+    }
+    return off;
+}
+
 __device__ __forceinline__ int64_t load_lid(const seg_u& s, uint32_t i)
 {
     if (s.lid64) return ((const GHX_GLOBAL int64_t*)(s.lids))[i];
@@ -180,22 +203,31 @@ __device__ __forceinline__ int64_t field_offset<seg_s>(const seg_s& s, uint32_t 
 
 // Copy one tile [start, end) of a segment. Lane-linear in buffer space: lanes of a wave touch
 // consecutive W-byte vectors of the buffer; kU independent vectors in flight per lane.
-template<bool PACK, int W, typename Seg>
+// AM: the segment's offset arithmetic (seg_s::amode): 0 general; 1 / 2 the short form, field
+// addressed as (field + field_off) + a 32-bit offset.
+template<bool PACK, int W, typename Seg, int AM = 0>
 __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field,
                                           char* __restrict__ buf, uint32_t start, uint32_t end)
 {
     using V = typename vec_t<W>::type;
     const uint32_t tid = threadIdx.x;
     const uint32_t pol = s.fpol;
+    if constexpr (AM != 0) field += s.field_off;
     for (uint32_t base = start + tid * W; base < end; base += kU * kBlock * W)
     {
         V v[kU];
-        int64_t fo[kU];
+        using off_t = std::conditional_t<AM == 0, int64_t, uint32_t>;
+        off_t fo[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u)
         {
             const uint32_t p = base + u * kBlock * W;
-            if (p < end) fo[u] = field_offset<Seg>(s, p);
+            if constexpr (AM == 0)
+            {
+                if (p < end) fo[u] = field_offset<Seg>(s, p);
+            }
+            else if (p < end)
+                fo[u] = field_offset_f<AM>(s, p);
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u)
@@ -569,6 +601,24 @@ __device__ __forceinline__ void copy_any(const Seg& s, char* field, char* buf, u
             unpack_tile_pipelined<16>(s, field, buf, start, end);
             return;
         }
+    if constexpr (std::is_same_v<Seg, seg_s>)
+    {
+        if (s.amode == 1)  // the short form for the widths fp32/fp64 fields give
+        {
+            switch (w)
+            {
+                case 4: copy_tile<PACK, 16, Seg, 1>(s, field, buf, start, end); return;
+                case 3: copy_tile<PACK, 8, Seg, 1>(s, field, buf, start, end); return;
+                case 2: copy_tile<PACK, 4, Seg, 1>(s, field, buf, start, end); return;
+                default: break;
+            }
+        }
+        else if (s.amode == 2 && w == 4)
+        {
+            copy_tile<PACK, 16, Seg, 2>(s, field, buf, start, end);
+            return;
+        }
+    }
     switch (w)
     {
         case 4: copy_tile<PACK, 16>(s, field, buf, start, end); break;
@@ -645,25 +695,40 @@ __global__ __launch_bounds__(kBlock) void k_copy(kargs a)
 // store. Every buffer byte and every halo byte is still written; what disappears is the
 // buffer read-back (which a lane-local read-back served from L2, or, for ~20 % of it, from HBM:
 // TCC_EA0_RDREQ 573k against 461k for the field reads alone).
-template<int W>
+// AM: 0 general; 1 both segments in the short form with one division (copy_tile's AM 1).
+template<int W, int AM = 0>
 __device__ __forceinline__ void self_forward(const seg_s& s, const seg_s& q,
                                              char* __restrict__ fp, char* __restrict__ fu,
                                              char* __restrict__ buf, uint32_t start, uint32_t end)
 {
     using V = typename vec_t<W>::type;
+    using off_t = std::conditional_t<AM == 0, int64_t, uint32_t>;
     const uint32_t pol_p = s.fpol, pol_u = q.fpol;
+    if constexpr (AM != 0)
+    {
+        fp += s.field_off;
+        fu += q.field_off;
+    }
     for (uint32_t base = start + threadIdx.x * W; base < end; base += kU * kBlock * W)
     {
         V v[kU];
-        int64_t op[kU], ou[kU];
+        off_t op[kU], ou[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u)
         {
             const uint32_t p = base + u * kBlock * W;
             if (p < end)
             {
-                op[u] = field_offset_s(s, p);
-                ou[u] = field_offset_s(q, p);
+                if constexpr (AM == 0)
+                {
+                    op[u] = field_offset_s(s, p);
+                    ou[u] = field_offset_s(q, p);
+                }
+                else
+                {
+                    op[u] = field_offset_f<AM>(s, p);
+                    ou[u] = field_offset_f<AM>(q, p);
+                }
             }
         }
 #pragma unroll
@@ -735,6 +800,12 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
             copy_any<true, kU>(s, field_p, buf, start, end, wp);
             continue;
         }
+        if (wp == wu && s.amode == 1 && q.amode == 1 && wp >= 3)
+        {
+            if (wp == 4) self_forward<16, 1>(s, q, field_p, field_u, buf, start, end);
+            else self_forward<8, 1>(s, q, field_p, field_u, buf, start, end);
+            continue;
+        }
         if (wp == wu)
         {
             switch (wp)
@@ -757,24 +828,38 @@ __global__ __launch_bounds__(kBlock) void k_self(kargs a)
 // Zero-copy put: element p of the virtual message is read from the source field through the
 // pack segment's addressing and written to the target field (peer memory or local) through the
 // unpack segment's addressing, register to register — no buffer.
-template<int W>
+template<int W, int AM = 0>
 __device__ __forceinline__ void copy_direct(const seg_s& s, const seg_s& q,
                                             const char* __restrict__ src, char* __restrict__ dst,
                                             uint32_t start, uint32_t end)
 {
     using V = typename vec_t<W>::type;
+    using off_t = std::conditional_t<AM == 0, int64_t, uint32_t>;
+    if constexpr (AM != 0)
+    {
+        src += s.field_off;
+        dst += q.field_off;
+    }
     for (uint32_t base = start + threadIdx.x * W; base < end; base += kU * kBlock * W)
     {
         V v[kU];
-        int64_t fd[kU];
+        off_t fd[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u)
         {
             const uint32_t p = base + u * kBlock * W;
             if (p < end)
             {
-                v[u] = vload<V>(src + field_offset_s(s, p));
-                fd[u] = field_offset_s(q, p);
+                if constexpr (AM == 0)
+                {
+                    v[u] = vload<V>(src + field_offset_s(s, p));
+                    fd[u] = field_offset_s(q, p);
+                }
+                else
+                {
+                    v[u] = vload<V>(src + field_offset_f<AM>(s, p));
+                    fd[u] = field_offset_f<AM>(q, p);
+                }
             }
         }
 #pragma unroll
@@ -816,6 +901,12 @@ __global__ __launch_bounds__(kBlock) void k_put(kargs a)
         int w = min(int(s.wlog2), int(q.wlog2));
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(src)));
         w = min(w, ptr_wlog2(reinterpret_cast<uint64_t>(dst)));
+        if (s.amode == 1 && q.amode == 1 && w >= 3)
+        {
+            if (w == 4) copy_direct<16, 1>(s, q, src, dst, start, end);
+            else copy_direct<8, 1>(s, q, src, dst, start, end);
+            continue;
+        }
         switch (w)
         {
             case 4: copy_direct<16>(s, q, src, dst, start, end); break;

@@ -95,6 +95,29 @@ uint32_t long_tile_bytes(const seg_u& s, int)
     return tb - tb % s.row_bytes;
 }
 
+// The short form of a segment's field-offset arithmetic (seg_s::amode, field_offset_f in
+// ghx_kernels.hip): a row's offset RELATIVE to field_off is computed in 32 bits from full-rate
+// 24-bit products (v_mul_u32_u24) with one division per outer dim beyond the last, instead of
+// the general form's three divisions and four int64 products (about 16 quarter-rate
+// multiplies per vector, the launch's VALU time at small shapes). Exact when every operand of a
+// product is below 2^24 and the relative offsets below 2^32: rows, row length, the decoded outer
+// extents and the strides (non-negative) of the outer dims in use.
+uint8_t short_addressing(const seg_s& s)
+{
+    if (!g_tune.fast_addr || s.n_outer > 3) return 0;
+    constexpr uint64_t k24 = uint64_t(1) << 24;
+    const uint64_t rows = s.row_bytes ? s.bytes / s.row_bytes : 0;
+    if (rows >= k24 || s.row_bytes >= k24) return 0;
+    uint64_t span = s.row_bytes;
+    for (int k = 0; k < s.n_outer; ++k)
+    {
+        if (s.stride[k] < 0 || uint64_t(s.stride[k]) >= k24 || s.ext[k] >= k24) return 0;
+        span += uint64_t(s.ext[k] - 1) * uint64_t(s.stride[k]);
+    }
+    if (span >= (uint64_t(1) << 32)) return 0;
+    return s.n_outer == 3 ? 2 : 1;
+}
+
 void set_pipe(seg_s& s, bool on) { s.pipe = on ? 1 : 0; }
 void set_pipe(seg_u&, bool) {}
 
@@ -462,6 +485,7 @@ uint64_t add_box_segments(std::vector<seg_s>& out, const ghx_field_desc& f, cons
         for (int k = 0; k < n_outer; ++k)
             if (s.ext[k] > 1) wf = std::min(wf, wlog2_of(uint64_t(s.stride[k] < 0 ? -s.stride[k] : s.stride[k])));
         s.wlog2 = uint8_t(std::min(wb, wf));
+        s.amode = short_addressing(s);
         out.push_back(s);
     }
     return uint64_t(n * elem);

@@ -20,6 +20,9 @@ def main():
     ap.add_argument("--shapes", default="")
     ap.add_argument("--tune", action="append", default=[])
     ap.add_argument("--no-floor", action="store_true", help="kernels only (no probes)")
+    ap.add_argument("--alone", action="store_true",
+                    help="also time each kernel back to back with itself (pack, pack, ...), the "
+                         "cache state the probes are timed in")
     a = ap.parse_args()
     shapes = [tuple(int(x) for x in sh.split(":")) for sh in a.shapes.split(",") if sh] or \
         [(N, H) for N in (256, 384, 512, 640) for H in (1, 2, 3)]
@@ -60,6 +63,12 @@ def main():
             def unpack(s):
                 _ghx.check(L.ghx_exchange_unpack(plan.h, fp, 1, sp, len(send), s), "unpack")
             kp, ku = bench.launch_durations(torch, dev, stream, _ghx, [pack, unpack])
+            alone = {}
+            if a.alone:
+                alone["pack_alone_us"] = round(
+                    bench.launch_durations(torch, dev, stream, _ghx, [pack])[0] * 1e6, 2)
+                alone["unpack_alone_us"] = round(
+                    bench.launch_durations(torch, dev, stream, _ghx, [unpack])[0] * 1e6, 2)
             torch.cuda.synchronize(dev)
             idx = (torch.arange(E, device=dev) - H) % N
             want = (idx.view(1, 1, E) + N * (idx.view(1, E, 1) + N * idx.view(E, 1, 1))).double()
@@ -75,7 +84,8 @@ def main():
                 "pack_floor_over_kernel": fl.get("floor_over_kernel"),
                 "unpack_floor_us": fl.get("write_floor", {}).get("floor_us"),
                 "unpack_floor_over_kernel": fl.get("write_floor", {}).get("floor_over_kernel"),
-                "xface_lines": fl.get("xface_lines"), "xface_only_us": fl.get("xface_only_us")}),
+                "xface_lines": fl.get("xface_lines"), "xface_only_us": fl.get("xface_only_us"),
+                **alone}),
                 flush=True)
             del f, want, send, co, bis, plan
             torch.cuda.empty_cache()

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Developer A/B (not product): the fused self exchange (k_self, the N=1 product exchange) and
-the two-launch step with tile records off / on (ghx_tune tile_records; the plans are rebuilt per
-setting), interleaved rounds, kernels' own events (bench.launch_durations, medians), one periodic
+the two-launch step with a 0/1 knob off / on (--knob, default tile_records; the plans are
+rebuilt per setting), interleaved rounds, kernels' own events (bench.launch_durations, medians), one periodic
 512^3 fp64 domain per halo width, every exchange verified. One JSON line per (round, setting, H).
-usage: python tools/self_rec_ab.py [--rounds 2] [--halos 1,2,3]"""
+usage: python tools/self_rec_ab.py [--rounds 2] [--halos 1,2,3] [--knob tile_records]"""
 import argparse
 import json
 import os
@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--halos", default="1,2,3")
     ap.add_argument("--N", type=int, default=512)
+    ap.add_argument("--knob", default="tile_records")
     a = ap.parse_args()
     import torch
 
@@ -31,7 +32,7 @@ def main():
     N = a.N
     for rnd in range(a.rounds):
         for rec in (0, 1) if rnd % 2 == 0 else (1, 0):
-            _ghx.call("ghx_tune", b"tile_records", rec)
+            _ghx.call("ghx_tune", a.knob.encode(), rec)
             for H in (int(h) for h in a.halos.split(",")):
                 E = N + 2 * H
                 ctx = ghex_amd.make_context()
@@ -64,7 +65,7 @@ def main():
                 fused(stream.cuda_stream)
                 torch.cuda.synchronize(dev)
                 ok = bool((f == want).all())
-                print(json.dumps({"round": rnd, "tile_records": rec, "N": N, "H": H,
+                print(json.dumps({"round": rnd, a.knob: rec, "N": N, "H": H,
                                   "self_us": round(ks * 1e6, 2), "pack_us": round(kp * 1e6, 2),
                                   "unpack_us": round(ku * 1e6, 2), "verified": ok}), flush=True)
                 del f, want, send, co, bis, plan
