@@ -3,7 +3,7 @@
 (tools/pmc_ifetch.sh): one periodic N^3 fp64 domain, halo H; `reps` pack launches, then `reps`
 unpack launches, then the pack's address-set probe (tools/pack_floor.hip k_lines), so that the
 per-kernel counters of the product launches and of the probe come from one process.
-usage: python tools/launch_anatomy.py N H [reps]"""
+usage: python tools/launch_anatomy.py N H [reps] [k=v,k=v (ghx_tune)]"""
 import os
 import sys
 
@@ -23,6 +23,9 @@ def main():
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream(dev).cuda_stream
     L = _ghx.lib()
+    for kv in filter(None, (sys.argv[4] if len(sys.argv) > 4 else "").split(",")):
+        k, v = kv.split("=")
+        _ghx.call("ghx_tune", k.encode(), int(v))
     E = N + 2 * H
     ctx = ghex_amd.make_context()
     dd = R.DomainDescriptor(0, (0, 0, 0), (N - 1,) * 3)

@@ -29,6 +29,8 @@ def main(d):
         if r.get("SQ_WAVES"):
             r["wave_cycles_per_wave"] = round(r.get("SQ_WAVE_CYCLES", 0) / r["SQ_WAVES"], 1)
             r["wait_inst_per_wave"] = round(r.get("SQ_WAIT_INST_ANY", 0) / r["SQ_WAVES"], 1)
+            if "SQ_ACTIVE_INST_VALU" in r:
+                r["valu_active_per_wave"] = round(r["SQ_ACTIVE_INST_VALU"] / r["SQ_WAVES"], 1)
     return out
 
 
