@@ -1254,16 +1254,18 @@ def index_floor(cells, levels, sends, recvs, k_gather, k_scatter):
 def multi_floor(N, H, elem_sizes, k_pack, k_unpack):
     """Config 4's address-set floors (tools/pack_floor.hip ghx_probe_multi_floor): the fields
     (element sizes `elem_sizes`) in one allocation at 2 MiB-aligned offsets. Pack: one 16-B load
-    per 128-B field line the pack reads (x-face lines first) + the buffer writes. Unpack: the
-    buffer read + every halo row's bytes written once (16/8/4-B pieces). Kernel-own events,
-    medians of 21, beside the product's pack / unpack launches (k_pack / k_unpack, seconds).
+    per 128-B field line the pack reads (x-face lines first) + the buffer writes. Unpack: every
+    halo row's bytes written once (16/8/4-B pieces from an address-ordered list), the write set
+    the unpack must issue (unpack_floor_us, as write_floor of pack_read_floor); with the buffer
+    read streamed first beside it (unpack_reads_writes_us). Kernel-own events, medians of 21,
+    beside the product's pack / unpack launches (k_pack / k_unpack, seconds).
     floor_over_kernel = probe time / product time (above 1: the product is faster)."""
     import ctypes
     try:
         L = _floor_lib()
         if L is None:
             return {"error": "tools/lib/libpackfloor.so not built (make -C tools)"}
-        us = (ctypes.c_double * 4)()
+        us = (ctypes.c_double * 6)()
         c = (ctypes.c_int64 * 3)()
         es = (ctypes.c_int * len(elem_sizes))(*elem_sizes)
         rc = L.ghx_probe_multi_floor(N, H, len(elem_sizes), es, 21, us, c)
@@ -1271,11 +1273,13 @@ def multi_floor(N, H, elem_sizes, k_pack, k_unpack):
             return {"error": f"HIP call failed at tools/pack_floor.hip:{rc}"}
         return {"lines": c[0], "pieces": c[1], "halo_bytes": c[2],
                 "pack_floor_us": round(us[0], 2), "pack_floor_cold_us": round(us[1], 2),
-                "unpack_floor_us": round(us[2], 2), "unpack_floor_cold_us": round(us[3], 2),
+                "unpack_floor_us": round(us[4], 2), "unpack_floor_cold_us": round(us[5], 2),
+                "unpack_reads_writes_us": round(us[2], 2),
+                "unpack_reads_writes_cold_us": round(us[3], 2),
                 "pack_kernel_us": round(k_pack * 1e6, 2),
                 "unpack_kernel_us": round(k_unpack * 1e6, 2),
                 "pack_floor_over_kernel": round(us[0] / (k_pack * 1e6), 3) if k_pack else None,
-                "unpack_floor_over_kernel": round(us[2] / (k_unpack * 1e6), 3)
+                "unpack_floor_over_kernel": round(us[4] / (k_unpack * 1e6), 3)
                 if k_unpack else None}
     except Exception as e:  # reported, never fatal
         return {"error": f"{type(e).__name__}: {str(e)[:200]}"}

@@ -3,7 +3,7 @@
 H=3) through bench.bench_config4 under plan-shaping ghx_tune settings: the verified two-launch
 step, the pack / unpack launches by their own events and the five-field floor probe
 (tools/pack_floor.hip ghx_probe_multi_floor). One JSON line per setting.
-usage: python tools/config4_sweep.py"""
+usage: python tools/config4_sweep.py [--settings JSON list of ghx_tune dicts]"""
 import json
 import os
 import sys
@@ -18,13 +18,18 @@ SETTINGS = [{}] + [{"small_tile_rows": r} for r in (256, 512, 1024)] + \
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--settings", default="")
+    a = ap.parse_args()
+    settings = json.loads(a.settings) if a.settings else SETTINGS
     import torch
     import bench
     import ghex_amd
     from ghex_amd import _ghx
     from ghex_amd.structured import regular as R
     dev = torch.device("cuda", 0)
-    for st in SETTINGS:
+    for st in settings:
         _ghx.call("ghx_tune", b"reset", 0)
         for k, v in st.items():
             _ghx.call("ghx_tune", k.encode(), v)
@@ -34,7 +39,9 @@ def main():
                           "verified": r["verified"], "pack_kernel_us": fl.get("pack_kernel_us"),
                           "unpack_kernel_us": fl.get("unpack_kernel_us"),
                           "pack_floor_us": fl.get("pack_floor_us"),
-                          "unpack_floor_us": fl.get("unpack_floor_us")}), flush=True)
+                          "unpack_floor_us": fl.get("unpack_floor_us"),
+                          "unpack_reads_writes_us": fl.get("unpack_reads_writes_us")}),
+              flush=True)
     _ghx.call("ghx_tune", b"reset", 0)
 
 

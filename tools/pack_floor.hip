@@ -611,8 +611,8 @@ __global__ __launch_bounds__(256) void k_pieces4(const uint32_t* __restrict__ pi
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
 }
 
-// out_us[4]: {pack floor warm, cold, unpack floor warm, cold}; counts[3]: lines, pieces, useful
-// bytes. Returns 0, or the failing source line.
+// out_us[6]: {pack floor warm, cold, unpack (buffer read + halo writes) warm, cold, halo writes
+// alone warm, cold}; counts[3]: lines, pieces, useful bytes. Returns 0, or the failing source line.
 extern "C" int ghx_probe_multi_floor(int N, int H, int n_fields, const int* es, int reps,
                                      double* out_us, int64_t* counts)
 {
@@ -660,7 +660,7 @@ extern "C" int ghx_probe_multi_floor(int N, int H, int n_fields, const int* es, 
     CK(hipMemset(fl, 2, flush_bytes));
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 3; ++j)
         for (int cold = 0; cold < 2; ++cold)
         {
             auto go = [&](hipEvent_t a, hipEvent_t b) {
@@ -668,10 +668,10 @@ extern "C" int ghx_probe_multi_floor(int N, int H, int n_fields, const int* es, 
                     hipExtLaunchKernelGGL(k_lines, dim3(grid), dim3(256), 0, 0, a, b, 0, d_l,
                                           uint32_t(lines.size()), (const char*)field, buf,
                                           uint64_t(useful / 16), sink);
-                else
+                else  // j = 2: the halo writes alone (the unpack's write set), no buffer read
                     hipExtLaunchKernelGGL(k_pieces4, dim3(grid), dim3(256), 0, 0, a, b, 0, d_p,
                                           uint32_t(pieces.size()), field, (const v4*)buf,
-                                          uint64_t(useful / 16), sink);
+                                          j == 1 ? uint64_t(useful / 16) : uint64_t(0), sink);
             };
             std::vector<float> t;
             for (int i = 0; i < reps; ++i)
