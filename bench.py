@@ -1327,8 +1327,12 @@ def pack_read_floor(N, Hw, roof):
                "xface_only_us": round(us[0], 2), "long_only_us": round(us[2], 2),
                "reads_us": round(us[4], 2), "reads_writes_us": round(us[6], 2),
                "reads_writes_cold_us": round(us[7], 2),
+               "reads_writes_dependent_us": round(us[8], 2),
+               "reads_writes_dependent_cold_us": round(us[9], 2),
                "pack_kernel_us": roof.get("pack_kernel_us"),
                "floor_over_kernel": round(us[6] / roof["pack_kernel_us"], 3)
+               if roof.get("pack_kernel_us") else None,
+               "dependent_over_kernel": round(us[8] / roof["pack_kernel_us"], 3)
                if roof.get("pack_kernel_us") else None}
         rc = L.ghx_probe_unpack_floor(N, Hw, 21, us, c)
         if rc:

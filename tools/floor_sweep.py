@@ -84,6 +84,8 @@ def main():
                 "pack_floor_over_kernel": fl.get("floor_over_kernel"),
                 "unpack_floor_us": fl.get("write_floor", {}).get("floor_us"),
                 "unpack_floor_over_kernel": fl.get("write_floor", {}).get("floor_over_kernel"),
+                "pack_floor_dependent_us": fl.get("reads_writes_dependent_us"),
+                "pack_dependent_over_kernel": fl.get("dependent_over_kernel"),
                 "xface_lines": fl.get("xface_lines"), "xface_only_us": fl.get("xface_only_us"),
                 **alone}),
                 flush=True)

@@ -44,7 +44,11 @@
 using v4 = unsigned __attribute__((ext_vector_type(4)));
 constexpr int kU = 4;
 
-// lines[0, n): one 16-B load per line; optionally the grid then streams `wbytes` of writes
+// lines[0, n): one 16-B load per line; optionally the grid then streams `wbytes` of writes.
+// DEP: every written vector carries a loaded value, so a lane's writes wait for its loads, as a
+// pack's buffer writes wait for the field reads they copy (the plain form's writes are
+// independent of its reads and overlap them freely).
+template<bool DEP = false>
 __global__ __launch_bounds__(256) void k_lines(const uint32_t* __restrict__ lines, uint32_t n,
                                                const char* __restrict__ field, v4* __restrict__ buf,
                                                uint64_t wvec, unsigned* sink)
@@ -61,7 +65,7 @@ __global__ __launch_bounds__(256) void k_lines(const uint32_t* __restrict__ line
             if (l[u] != 0xffffffffu) acc ^= *(const v4*)(field + uint64_t(l[u]) * 128);
     }
     for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < wvec; i += uint64_t(stride))
-        buf[i] = v4{unsigned(i), 1, 2, 3};
+        buf[i] = v4{unsigned(i), DEP ? acc.x : 1u, 2, 3};
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[0] = acc.x;
 }
 
@@ -305,7 +309,8 @@ done:
     return rc;
 }
 
-// out_us[8]: {xface, long, both, both_rw} x {warm, cold} (microseconds, kernel-own events);
+// out_us[10]: {xface, long, both, both_rw, both_rw with dependent writes} x {warm, cold}
+// (microseconds, kernel-own events);
 // counts[3]: x-face lines, long-row lines, useful bytes. Returns 0, or the failing source line.
 extern "C" int ghx_probe_pack_floor(int N, int H, int reps, double* out_us, int64_t* counts)
 {
@@ -341,10 +346,10 @@ extern "C" int ghx_probe_pack_floor(int N, int H, int reps, double* out_us, int6
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     {
-        const uint32_t* lists[4] = {d_xf, d_lg, d_both, d_both};
-        const size_t ns[4] = {xf.size(), lg.size(), both.size(), both.size()};
-        const uint64_t wv[4] = {0, 0, 0, useful / 16};
-        for (int j = 0; j < 4; ++j)
+        const uint32_t* lists[5] = {d_xf, d_lg, d_both, d_both, d_both};
+        const size_t ns[5] = {xf.size(), lg.size(), both.size(), both.size(), both.size()};
+        const uint64_t wv[5] = {0, 0, 0, useful / 16, useful / 16};
+        for (int j = 0; j < 5; ++j)
             for (int cold = 0; cold < 2; ++cold)
             {
                 std::vector<float> t;
@@ -353,11 +358,19 @@ extern "C" int ghx_probe_pack_floor(int N, int H, int reps, double* out_us, int6
                     if (cold)
                         hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, 0, (const v4*)fl,
                                            flush_bytes / 16, sink);
+                    else if (j == 4)
+                        hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(256), 0, 0, lists[j],
+                                           uint32_t(ns[j]), (const char*)field, buf, wv[j], sink);
                     else
-                        hipLaunchKernelGGL(k_lines, dim3(grid), dim3(256), 0, 0, lists[j], uint32_t(ns[j]),
+                        hipLaunchKernelGGL(k_lines<>, dim3(grid), dim3(256), 0, 0, lists[j], uint32_t(ns[j]),
                                            (const char*)field, buf, wv[j], sink);
-                    hipExtLaunchKernelGGL(k_lines, dim3(grid), dim3(256), 0, 0, e0, e1, 0, lists[j],
-                                          uint32_t(ns[j]), (const char*)field, buf, wv[j], sink);
+                    if (j == 4)
+                        hipExtLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(256), 0, 0, e0, e1, 0,
+                                              lists[j], uint32_t(ns[j]), (const char*)field, buf,
+                                              wv[j], sink);
+                    else
+                        hipExtLaunchKernelGGL(k_lines<>, dim3(grid), dim3(256), 0, 0, e0, e1, 0, lists[j],
+                                              uint32_t(ns[j]), (const char*)field, buf, wv[j], sink);
                     CK(hipEventSynchronize(e1));
                     float ms = 0;
                     CK(hipEventElapsedTime(&ms, e0, e1));
@@ -665,7 +678,7 @@ extern "C" int ghx_probe_multi_floor(int N, int H, int n_fields, const int* es, 
         {
             auto go = [&](hipEvent_t a, hipEvent_t b) {
                 if (j == 0)
-                    hipExtLaunchKernelGGL(k_lines, dim3(grid), dim3(256), 0, 0, a, b, 0, d_l,
+                    hipExtLaunchKernelGGL(k_lines<>, dim3(grid), dim3(256), 0, 0, a, b, 0, d_l,
                                           uint32_t(lines.size()), (const char*)field, buf,
                                           uint64_t(useful / 16), sink);
                 else  // j = 2: the halo writes alone (the unpack's write set), no buffer read
