@@ -39,6 +39,8 @@ struct tuning
                                        // H=3 32.8 vs 32.0 (profiles/r01c_fwd_tile_ab.jsonl)
     uint32_t small_tile_rows = 0;      // rows per tile of segments with short rows (0: by the
                                        // plan's short-row count, ghx_plan.cpp short_tile_rows)
+    uint32_t pack_tile_rows = 0;       // rows per short-row tile of PACK plans only (0: as
+                                       // small_tile_rows / the plan's rule)
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
     uint32_t u_tile_bytes = 16384;     // tile of unstructured segments with long rows (config 5's

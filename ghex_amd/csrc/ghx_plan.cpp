@@ -71,15 +71,23 @@ std::vector<int32_t> line_partners(const std::vector<seg_u>& segs)
 // was 15-17 % slower at 512^3 H=1/H=3 than 2048 rows. Index-list gathers are latency-bound
 // random accesses and want many workgroups in flight (512 rows), except run-heavy lists on the
 // run path, which stream (2048 rows: tools/urun_bench.py, contiguous lids 40 -> 33 us).
-uint32_t short_tile_rows(const seg_s& s, uint64_t short_rows)
+// Pack plans whose short rows take several vector accesses each (24-B rows of fp64 at H=3, 12-B
+// rows of fp32) cut four times finer (round 6): the pack at 384^3 / 512^3 / 640^3 H=3 takes 12.6 ->
+// 11.5 / 19.7 -> 18.5 / 34.3 -> 31.8-33.9 us with 512-row tiles against the old rule's 1024-2048
+// rows, 256^3 H=3 equal; single-access rows (H=1, H=2 fp64) keep the old rule, which wins there
+// (interleaved A/B, profiles/r06an_pack_tile_rows_ab.jsonl; sweep r06am_pack_tile_rows_sweep.jsonl).
+uint32_t short_tile_rows(const seg_s& s, uint64_t short_rows, int dir)
 {
+    if (dir == 0 && g_tune.pack_tile_rows) return g_tune.pack_tile_rows;
     if (g_tune.small_tile_rows) return g_tune.small_tile_rows;
-    const uint64_t want = short_rows / (s.row_bytes == 16 ? 128 : 256);
+    // several vector accesses per row (whatever the pointers' alignment allows)
+    const bool multi = s.row_bytes > 16 || (s.row_bytes & (s.row_bytes - 1)) != 0;
+    const uint64_t want = short_rows / (dir == 0 && multi ? 1024 : s.row_bytes == 16 ? 128 : 256);
     uint32_t r = 512;
     while (r < 4096 && uint64_t(r) * 2 <= want) r *= 2;
     return r;
 }
-uint32_t short_tile_rows(const seg_u& s, uint64_t)
+uint32_t short_tile_rows(const seg_u& s, uint64_t, int)
 {
     return s.runs == 2 ? g_tune.u_run_tile_rows : g_tune.u_tile_rows;
 }
@@ -141,7 +149,7 @@ std::vector<uint32_t> build_tiles(std::vector<Seg>& segs, int dir)
         uint32_t tb = long_tile_bytes(segs[i], dir);
         if (small)
         {
-            const uint32_t rows = short_tile_rows(segs[i], short_rows[segs[i].field_slot]);
+            const uint32_t rows = short_tile_rows(segs[i], short_rows[segs[i].field_slot], dir);
             const uint64_t want = uint64_t(rows) * segs[i].row_bytes;
             tb = uint32_t(std::max<uint64_t>(segs[i].row_bytes, std::min<uint64_t>(want, kMaxTileBytes)));
             tb -= tb % segs[i].row_bytes;  // whole rows per tile
