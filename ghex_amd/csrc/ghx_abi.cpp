@@ -521,6 +521,12 @@ int ghx_tune(const char* key, int32_t value)
                 throw invalid("pack_tile_rows must be 0 (as small_tile_rows) or in [64, 65536]");
             g_tune.pack_tile_rows = uint32_t(value);
         }
+        else if (k == "unpack_tile_rows")
+        {
+            if (value != 0 && (value < 64 || value > 65536))
+                throw invalid("unpack_tile_rows must be 0 (as small_tile_rows) or in [64, 65536]");
+            g_tune.unpack_tile_rows = uint32_t(value);
+        }
         else if (k == "fast_addr")
         {
             if (value < 0 || value > 1) throw invalid("fast_addr must be 0 or 1");

@@ -41,6 +41,7 @@ struct tuning
                                        // plan's short-row count, ghx_plan.cpp short_tile_rows)
     uint32_t pack_tile_rows = 0;       // rows per short-row tile of PACK plans only (0: as
                                        // small_tile_rows / the plan's rule)
+    uint32_t unpack_tile_rows = 0;     // the same for UNPACK plans
     uint32_t small_row_bytes = 64;     // rows shorter than this are "short" (request-bound)
     uint32_t u_tile_rows = 512;        // rows per tile of short-row unstructured segments
     uint32_t u_tile_bytes = 16384;     // tile of unstructured segments with long rows (config 5's

@@ -79,6 +79,7 @@ std::vector<int32_t> line_partners(const std::vector<seg_u>& segs)
 uint32_t short_tile_rows(const seg_s& s, uint64_t short_rows, int dir)
 {
     if (dir == 0 && g_tune.pack_tile_rows) return g_tune.pack_tile_rows;
+    if (dir == 1 && g_tune.unpack_tile_rows) return g_tune.unpack_tile_rows;
     if (g_tune.small_tile_rows) return g_tune.small_tile_rows;
     // several vector accesses per row (whatever the pointers' alignment allows)
     const bool multi = s.row_bytes > 16 || (s.row_bytes & (s.row_bytes - 1)) != 0;
