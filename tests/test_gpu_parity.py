@@ -416,7 +416,8 @@ def test_full_size_512_h2_checksum():
                                    {"unpack_tile_bytes": 32768},
                                    {"unpack_tile_bytes": 16384, "tile_records": 0},
                                    {"fast_addr": 0}, {"fast_addr": 0, "tile_records": 0},
-                                   {"pack_tile_rows": 64}],
+                                   {"pack_tile_rows": 64}, {"unpack_tile_rows": 64},
+                                   {"pack_tile_rows": 4096, "unpack_tile_rows": 128}],
                          ids=lambda d: "-".join(f"{k}={v}" for k, v in d.items()))
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_tuning_variants_stay_bit_exact(knobs, Hw):

@@ -107,7 +107,8 @@ def fused_vs_unfused(Hw, layout, N):
                                    {"self_tile_bytes": 2048, "grid_cap": 5},
                                    {"self_tile_bytes": 65536, "xcd_pair": 0},
                                    {"short_pol": 3}, {"tile_records": 0},
-                                   {"self_tile_bytes": 4096, "tile_records": 0, "grid_cap": 5}])
+                                   {"self_tile_bytes": 4096, "tile_records": 0, "grid_cap": 5},
+                                   {"fast_addr": 0}, {"pack_tile_rows": 64}])
 @pytest.mark.parametrize("Hw", [1, 2, 3])
 def test_self_kernel_variants_stay_bit_exact(knobs, Hw):
     """The fused self kernel under its remaining knobs (tile sizes, a grid-stride loop, XCD

@@ -47,6 +47,25 @@ def test_errors_are_reported_not_thrown(ghx):
     assert b"null" in ghx.lib().ghx_last_error() or b"dim" in ghx.lib().ghx_last_error()
 
 
+@pytest.mark.parametrize("key,good,bad", [("fast_addr", [0, 1], [-1, 2]),
+                                           ("pack_tile_rows", [0, 64, 65536], [-1, 63, 65537]),
+                                           ("unpack_tile_rows", [0, 512], [32, 1 << 20]),
+                                           ("tile_records", [0, 1], [2])])
+def test_tuning_knobs_validate_their_range(ghx, key, good, bad):
+    """ghx_tune accepts each knob's documented range and refuses the rest with a message naming
+    the knob (unknown keys too); `reset` restores the defaults."""
+    L = ghx.lib()
+    try:
+        for v in good:
+            assert L.ghx_tune(key.encode(), v) == 0, (key, v, L.ghx_last_error())
+        for v in bad:
+            assert L.ghx_tune(key.encode(), v) != 0, (key, v)
+            assert key.encode() in L.ghx_last_error()
+        assert L.ghx_tune(b"no_such_knob", 1) != 0
+    finally:
+        assert L.ghx_tune(b"reset", 0) == 0
+
+
 def test_halo_boxes_via_abi_match_reference(golden_dir):
     from ghex_amd.structured.regular import DomainDescriptor, HaloGenerator
     with open(os.path.join(golden_dir, "ref_halo_boxes.json")) as fh:
