@@ -205,7 +205,7 @@ __device__ __forceinline__ int64_t field_offset<seg_s>(const seg_s& s, uint32_t 
 // consecutive W-byte vectors of the buffer; kU independent vectors in flight per lane.
 // AM: the segment's offset arithmetic (seg_s::amode): 0 general; 1 / 2 the short form, field
 // addressed as (field + field_off) + a 32-bit offset.
-template<bool PACK, int W, typename Seg, int AM = 0>
+template<bool PACK, int W, typename Seg, int AM = 0, int kU = ghx::kU>
 __device__ __forceinline__ void copy_tile(const Seg& s, char* __restrict__ field,
                                           char* __restrict__ buf, uint32_t start, uint32_t end)
 {
@@ -607,9 +607,9 @@ __device__ __forceinline__ void copy_any(const Seg& s, char* field, char* buf, u
         {
             switch (w)
             {
-                case 4: copy_tile<PACK, 16, Seg, 1>(s, field, buf, start, end); return;
-                case 3: copy_tile<PACK, 8, Seg, 1>(s, field, buf, start, end); return;
-                case 2: copy_tile<PACK, 4, Seg, 1>(s, field, buf, start, end); return;
+                case 4: copy_tile<PACK, 16, Seg, 1, UU>(s, field, buf, start, end); return;
+                case 3: copy_tile<PACK, 8, Seg, 1, UU>(s, field, buf, start, end); return;
+                case 2: copy_tile<PACK, 4, Seg, 1, UU>(s, field, buf, start, end); return;
                 default: break;
             }
         }
