@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Developer measurement (not product): a short program to run under rocprofv3 --pmc
-(tools/pmc_ifetch.sh): one periodic N^3 fp64 domain, halo H; `reps` pack launches, then `reps`
-unpack launches, then the pack's address-set probe (tools/pack_floor.hip k_lines), so that the
-per-kernel counters of the product launches and of the probe come from one process.
+(tools/pmc_ifetch.sh): one periodic N^3 fp64 domain, halo H; `reps` pack + unpack steps, then
+`reps` pack launches back to back, then `reps` unpack launches, then the pack's address-set probe
+(tools/pack_floor.hip k_lines: per variant j = 0..4 2*5 warm launches and 5 after a cache sweep),
+so that the per-kernel counters of the product launches and of the probe come from one process
+(tools/parse_pmc_l2.py splits them by position).
 usage: python tools/launch_anatomy.py N H [reps] [k=v,k=v (ghx_tune)]"""
 import os
 import sys
@@ -37,7 +39,10 @@ def main():
     send, _ = co.buffers(plan, dev)
     fp = _ghx.ptr_array([f.data_ptr()])
     sp = _ghx.ptr_array([t.data_ptr() for t in send])
-    for _ in range(reps):
+    for _ in range(reps):  # the step: pack, unpack, pack, ... (launches 0..2*reps-1)
+        _ghx.check(L.ghx_exchange_pack(plan.h, fp, 1, sp, len(send), s), "pack")
+        _ghx.check(L.ghx_exchange_unpack(plan.h, fp, 1, sp, len(send), s), "unpack")
+    for _ in range(reps):  # then each alone, back to back
         _ghx.check(L.ghx_exchange_pack(plan.h, fp, 1, sp, len(send), s), "pack")
     for _ in range(reps):
         _ghx.check(L.ghx_exchange_unpack(plan.h, fp, 1, sp, len(send), s), "unpack")
