@@ -50,6 +50,9 @@ def _export_probe(tag, t):
           f"{L.ghx_last_error().decode()[:100] if rc else ''}", flush=True)
 
 
+_kept = []
+
+
 def main():
     px, py, pz, N, Hw = (int(v) for v in sys.argv[1:6])
     reps = int(sys.argv[6]) if len(sys.argv) > 6 else 3
@@ -80,6 +83,7 @@ def main():
     probe = os.environ.get("GHX_WORKER_EXPORT_PROBE") == "1"  # developer diagnosis
     if probe:
         _export_probe("start", torch.empty((N + 2 * Hw,) * 3, dtype=torch.float64, device="cuda"))
+    co = None
     for layout in [(2, 1, 0), (0, 2, 1)]:
         a, _ = H.linear_index_field(dom, N, Hw, gl, layout=layout)
         if probe:
@@ -90,6 +94,36 @@ def main():
             _export_probe("after_expect_numpy", torch.empty(a.shape, dtype=torch.float64,
                                                             device="cuda"))
         base, logical = device_field(a, layout)
+        if os.environ.get("GHX_DIAG_SYNC") == "1":  # developer diagnosis: export after a sync
+            torch.cuda.synchronize()
+        part = os.environ.get("GHX_DIAG_TEARDOWN", "")  # developer diagnosis: one teardown part
+        if part and layout != (2, 1, 0) and co is not None:
+            from ghex_amd import _ghx as G
+            import ctypes as C
+            if part == "imports":
+                for b in co._imports:
+                    G.lib().ghx_ipc_close(C.c_void_p(b))
+                co._imports = []
+            elif part == "puts":
+                for h, *_ in co._puts:
+                    G.lib().ghx_put_destroy(h)
+                co._puts = []
+            elif part == "epochs" and co._ep is not None:
+                G.lib().ghx_epochs_destroy(co._ep)
+                co._ep = None
+            elif part == "free":
+                junk = torch.empty(1 << 22, dtype=torch.float64, device="cuda")
+                del junk
+                torch.cuda.empty_cache()
+            _export_probe(f"after_{part}", base)
+        prime = os.environ.get("GHX_DIAG_PRIME", "0")  # developer diagnosis: exports first
+        if prime in ("1", "small"):
+            _export_probe("prime_small", torch.empty(1 << 18, dtype=torch.float64, device="cuda"))
+        if prime in ("1", "big"):
+            _export_probe("prime_field_size", torch.empty(a.shape, dtype=torch.float64,
+                                                          device="cuda"))
+        if prime == "self":
+            _export_probe("prime_self", base)
         if probe:
             _export_probe("field", base)
         fd = R.make_field_descriptor(dd, logical, (Hw,) * 3, (N + 2 * Hw,) * 3)
@@ -277,7 +311,18 @@ def main():
             for _ in range(reps):
                 co.exchange([pc(fd)]).wait()
         got = base.cpu().numpy()
-        bad += int(np.count_nonzero(got != expect))
+        if os.environ.get("GHX_DIAG_KEEPCO") == "1":  # developer diagnosis: no teardown
+            _kept.append((co, base))
+        if os.environ.get("GHX_DIAG_BARRIER") == "1":  # developer diagnosis: ordered teardown
+            torch.cuda.synchronize()
+            dist.barrier()
+            del co
+            import gc
+            gc.collect()
+            dist.barrier()
+            co = None
+        nb = int(np.count_nonzero(got != expect))
+        bad += nb
     t = torch.tensor([bad])
     dist.all_reduce(t)
     if rank == 0:
