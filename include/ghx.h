@@ -59,6 +59,9 @@ typedef void* ghx_stream;
  * workgroup index instead of a tile table entry and then its segment; default 1),
  * "unpack_tile_bytes" (0 = tile_bytes, the default; else the long-row tile of unpack plans, whose
  * tiles of several steps the unpack kernel then software-pipelines);
+ * "fast_addr" (0|1: short-form 32-bit field addressing for segments whose extents, strides and
+ * span fit it; default 1), "pack_tile_rows" / "unpack_tile_rows" (0 = by the plan's rule, the
+ * default; else 64..65536 rows per tile of short-row structured segments of pack / unpack plans);
  * "reset" restores every default. Plan-shaping knobs apply to plans created afterwards. Unknown
  * keys fail with GHX_ERR_INVALID (the variants removed in round 3 are listed in
  * tools/kernel_variants_r02.hip).
